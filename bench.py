@@ -1,0 +1,236 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X r2iq DDC hot path (BASELINE.json metric).
+
+metric : input MSamples/s at decim=2 (d=0) + achieved % HBM roofline, 1 GPU; IQ max-rel-err
+config : configs[1] "single-channel DDC, 128 MS/s int16 in, decim=2, 1xMI355X"
+step   : one pass of the fused frame kernel over one batch of --nblk blocks
+         (default 2048 x 65536 int16 = 256 MiB, resident in HBM before timing)
+
+  python bench.py [--gpus N --steps K --warmup W] [--d 0] [--mode single|channels]
+
+N > 1 (launched by torch.distributed.run, one rank per GPU):
+  single   : weak scaling — each rank owns its own time segment of the stream
+             (independent blocks + their 4096-sample halo; no data-path collective)
+  channels : config C5 — one 128 MS/s stream, 1024 tune bins sharded over the
+             ranks, the int16 batch broadcast from rank 0 over xGMI (RCCL) every step
+Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+BLOCK = 65536
+HALF = 4096
+
+
+def algorithmic_bytes_per_sample(d: int, nch: int = 1) -> float:
+    """B(d) = 2 B int16 read + 8 B per output complex / 2^(d+1) input samples, per channel
+    (SURVEY.md §8(d)); the 4/3 frame overlap and the tables are not counted."""
+    return 2.0 + nch * 8.0 / (1 << (d + 1))
+
+
+def make_input(torch, nblk: int, seed: int, device) -> "torch.Tensor":
+    """Synthetic 128 MS/s-labelled tone mix + noise (SURVEY.md §8(d) source (i)), int16 in HBM."""
+    n = nblk * BLOCK
+    g = torch.Generator(device=device).manual_seed(seed)
+    t = torch.arange(n, dtype=torch.float64, device=device)
+    x = 9000 * torch.sin(2 * np.pi * 0.0713 * t) + 3000 * torch.sin(2 * np.pi * 0.191 * t)
+    del t
+    x += 300 * torch.randn(n, dtype=torch.float64, device=device, generator=g)
+    out = torch.zeros(HALF + n, dtype=torch.int16, device=device)
+    out[HALF:] = x.round().clamp_(-32768, 32767).to(torch.int16)
+    del x
+    return out
+
+
+def cpu_baseline(d: int, tunebin: int, gpu_sample_out, sample_in: np.ndarray, nblk_sample: int,
+                 budget_s: float) -> dict:
+    """Time the oracle's float32 port (oracle/ddc_oracle.c, kind "port") on this host, 1 thread,
+    on a bounded sample of the same workload; also check the GPU output on that sample."""
+    sys.path.insert(0, ROOT)
+    from oracle import oracle as O
+    H32 = O.filter_bank(1.0, np.float32)
+    O.r2iq(sample_in, 1, d, tunebin, dtype=np.float32, H=H32)      # warm tables
+    done, t0 = 0, time.perf_counter()
+    while True:
+        O.r2iq(sample_in, nblk_sample, d, tunebin, dtype=np.float32, H=H32)
+        done += nblk_sample
+        if time.perf_counter() - t0 >= budget_s:
+            break
+    dt = time.perf_counter() - t0
+    ref = O.r2iq(sample_in, nblk_sample, d, tunebin)                # f64 checker
+    err = O.max_rel_err(gpu_sample_out, ref)
+    cpu = "unknown"
+    try:
+        for line in subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout.splitlines():
+            if line.startswith("Model name"):
+                cpu = line.split(":", 1)[1].strip()
+    except Exception:
+        pass
+    return {
+        "value": done * BLOCK / dt / 1e6, "unit": "input MSamples/s", "cores": 1, "kind": "port",
+        "sample": f"{nblk_sample} blocks x 65536 int16 (tone mix), repeated for {dt:.1f} s, "
+                  f"d={d}, tunebin={tunebin}, float32 oracle port, 1 thread",
+        "cpu_model": cpu, "host_nproc": os.cpu_count(),
+        "iq_max_rel_err_gpu_vs_oracle_f64": err,
+        "iq_rms_rel_err_gpu_vs_oracle_f64": O.rms_rel_err(gpu_sample_out, ref),
+    }
+
+
+def load_traffic(workload: str):
+    """Per-launch HBM bytes measured with rocprofv3 --pmc (profiles/pmc_traffic.json), if present."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(p) as f:
+            return json.load(f).get(workload)
+    except Exception:
+        return None
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--d", type=int, default=0, help="decimation index (0 = decim 2)")
+    ap.add_argument("--tunebin", type=int, default=1024)
+    ap.add_argument("--nblk", type=int, default=2048, help="blocks of 65536 per step per GPU")
+    ap.add_argument("--mode", choices=["single", "channels"], default="single")
+    ap.add_argument("--channels", type=int, default=1024)
+    ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds of CPU-baseline work")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    from extio_sddc_amd import R2iq, output_samples
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+
+    d, nblk = args.d, args.nblk
+    ddc = R2iq(gain=1.0, device=local)
+    ddc.setDecimate(d)
+    ddc.setTuneBin(args.tunebin)
+    stream = torch.cuda.current_stream()
+
+    if args.mode == "single":
+        # weak scaling: rank r owns stream segment r (its own blocks + halo)
+        d_in = make_input(torch, nblk, 0x5DDC + rank, dev)
+        d_out = torch.empty(output_samples(d, nblk) * 2, dtype=torch.float32, device=dev)
+        nch_local = 1
+
+        def step():
+            ddc.process_device(d_in, nblk, d_out, stream)
+        samples_per_step_all = nblk * BLOCK * world
+        workload = f"single d={d} nblk={nblk}"
+    else:
+        from extio_sddc_amd.shard import channel_shard
+        tbs_all = [4 * c for c in range(args.channels)]
+        lo, hi = channel_shard(args.channels, world, rank)
+        tbs = tbs_all[lo:hi]
+        nch_local = len(tbs)
+        d_in = make_input(torch, nblk, 0x5DDC, dev) if rank == 0 else \
+            torch.empty(HALF + nblk * BLOCK, dtype=torch.int16, device=dev)
+        per = output_samples(d, nblk) * 2
+        d_out = torch.empty((nch_local, per), dtype=torch.float32, device=dev)
+
+        def step():
+            if world > 1:
+                dist.broadcast(d_in, src=0)
+            ddc.process_channels_device(d_in, nblk, tbs, d_out, stream)
+        samples_per_step_all = nblk * BLOCK          # one shared stream
+        workload = f"channels d={d} nblk={nblk} nch={args.channels}"
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    kern_ms = ev0.elapsed_time(ev1) / args.steps          # per step on the launch stream
+    t = torch.tensor([wall, kern_ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall, kern_ms = t.tolist()
+
+    value = samples_per_step_all * args.steps / wall / 1e6
+    # roofline of the dominant kernel on THIS rank's launch
+    alg_bytes = nblk * BLOCK * algorithmic_bytes_per_sample(d, nch_local)
+    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    traffic = load_traffic(workload)
+
+    result = {
+        "metric": "input MSamples/s at decim=2 + achieved % HBM roofline, 1 GPU; IQ max-rel-err",
+        "value": value, "unit": "input MSamples/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": wall * 1e3 / args.steps, "higher_is_better": True,
+        "scaling": "weak" if args.mode == "single" else "strong",
+        "vs_baseline": None, "dtype": "f32 (int16 in, complex64 out)", "data": "synthetic",
+        "config": {"workload": "single-channel DDC, 128 MS/s int16 in, decim=2, 1xMI355X"
+                   if (args.mode == "single" and d == 0) else workload,
+                   "decim": 2 << d, "d": d, "tunebin": args.tunebin, "blocks_per_step_per_gpu": nblk,
+                   "block_samples": BLOCK, "mode": args.mode,
+                   "channels": args.channels if args.mode == "channels" else 1,
+                   "parallelism": f"time-segments x{world}" if args.mode == "single" else f"channels x{world}"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": "r2iq_frame_kernel" if args.mode == "single" else "r2iq_channels_kernel",
+                     "kernel_ms_per_launch": kern_ms,
+                     "algorithmic_bytes_per_launch": alg_bytes,
+                     "bytes_per_input_sample": algorithmic_bytes_per_sample(d, nch_local)},
+    }
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        ns = 16
+        sample = d_in[: HALF + ns * BLOCK].cpu().numpy()
+        if args.mode == "single":
+            gout = d_out[: output_samples(d, ns) * 2].cpu().numpy().view(np.complex64)
+            tb = args.tunebin
+        else:
+            gout = d_out[0, : output_samples(d, ns) * 2].cpu().numpy().view(np.complex64)
+            tb = tbs[0]
+        # d_out holds the whole batch; its first ns blocks depend only on the first ns blocks
+        cb = cpu_baseline(d, tb, gout, sample, ns, args.cpu_budget)
+        result["cpu_baseline"] = cb
+        result["iq_max_rel_err"] = cb.pop("iq_max_rel_err_gpu_vs_oracle_f64")
+        result["iq_rms_rel_err"] = cb.pop("iq_rms_rel_err_gpu_vs_oracle_f64")
+    if rank == 0:
+        result["host"] = platform.node()
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,352 @@
+// ddc_runtime.cpp — implementation of the C ABI in include/sddc_ddc.h.
+//
+// Owns the per-handle device state that the reference keeps in fft_mt_r2iq
+// (Core/fft_mt_r2iq.h:86-117): the filter bank (filterHw), the FFT "plans"
+// (here: twiddle tables), the tune bin and the stream history.  There is no CPU
+// fallback: every compute call goes to the gfx950 kernels in ddc_kernels.hip.
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <cmath>
+#include <complex>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "ddc_kernels.h"
+#include "filterbank.h"
+#include "sddc_ddc.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const char *fmt, ...)
+{
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                         \
+    do {                                                                                      \
+        hipError_t e_ = (expr);                                                               \
+        if (e_ != hipSuccess)                                                                 \
+            return fail(SDDC_ERR_HIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_),  \
+                        __FILE__, __LINE__);                                                  \
+    } while (0)
+
+// Restores the caller's current device on scope exit (torch and other users of
+// the same process keep their own current device).
+struct DeviceGuard {
+    int prev = -1;
+    hipError_t err = hipSuccess;
+    explicit DeviceGuard(int dev)
+    {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) err = hipSetDevice(dev);
+    }
+    ~DeviceGuard()
+    {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+constexpr int kHistory = SDDC_DDC_HALF_FFT;
+constexpr int kBlock = SDDC_DDC_BLOCK;
+constexpr int kHostChunk = 64;   // blocks per H2D/kernel/D2H round on the host path
+
+}  // namespace
+
+struct sddc_ddc {
+    int device = 0;
+    float gain = 0.f;
+    int d = 0, lsb = 0, rand = 0, tunebin = SDDC_DDC_HALF_FFT / 4;   // ctor: mtunebin = halfFft/4
+    sddc::KernelTables tables;
+    float2 *d_tables = nullptr;
+
+    std::mutex mu;                         // serialises the host path and buffer growth
+    hipStream_t stream = nullptr;          // host-path stream
+    int16_t *h_in = nullptr;               // pinned [history | chunk]
+    float *h_out = nullptr;                // pinned
+    int16_t *d_in = nullptr;
+    float *d_out = nullptr;
+
+    int *d_tunebins = nullptr;             // channel tune bins (device)
+    std::vector<int> tunebins_cached;
+};
+
+extern "C" {
+
+int sddc_ddc_abi_version(void) { return SDDC_DDC_ABI_VERSION; }
+
+const char *sddc_ddc_last_error(void) { return g_last_error.c_str(); }
+
+int sddc_ddc_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int sddc_ddc_kaiser(int ntaps, float astop, float fpass, float fstop, float *coef)
+{
+    return sddc::kaiser_window(ntaps, astop, fpass, fstop, coef);
+}
+
+int sddc_ddc_filter_taps(int d, float *taps)
+{
+    if (d < 0 || d >= SDDC_DDC_NDEC || !taps) return fail(SDDC_ERR_ARG, "filter_taps: bad d=%d or null", d);
+    sddc::filter_taps(d, taps);
+    return SDDC_OK;
+}
+
+int sddc_ddc_filter_response(float gain, int d, float *H)
+{
+    if (d < 0 || d >= SDDC_DDC_NDEC || !H) return fail(SDDC_ERR_ARG, "filter_response: bad d=%d or null", d);
+    std::vector<std::complex<double>> h(SDDC_DDC_HALF_FFT);
+    sddc::filter_response(gain, d, h.data());
+    for (int i = 0; i < SDDC_DDC_HALF_FFT; i++) {
+        H[2 * i] = (float)h[i].real();
+        H[2 * i + 1] = (float)h[i].imag();
+    }
+    return SDDC_OK;
+}
+
+size_t sddc_ddc_output_samples(int d, int nblk)
+{
+    if (d < 0 || d >= SDDC_DDC_NDEC || nblk < 0) return 0;
+    return (size_t)nblk * (size_t)(SDDC_DDC_OUT_BLOCK >> d);
+}
+
+int sddc_ddc_create(float gain, int device, sddc_ddc_t **out)
+{
+    if (!out) return fail(SDDC_ERR_ARG, "create: null out");
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+        return fail(SDDC_ERR_NODEV, "create: no HIP device visible");
+    if (device < 0 || device >= ndev) return fail(SDDC_ERR_NODEV, "create: device %d of %d", device, ndev);
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(SDDC_ERR_NODEV, "create: device %d is %s, the kernels are built for gfx950", device,
+                    prop.gcnArchName);
+
+    DeviceGuard g(device);
+    HIP_TRY(g.err);
+
+    auto *h = new (std::nothrow) sddc_ddc();
+    if (!h) return fail(SDDC_ERR_NOMEM, "create: out of host memory");
+    h->device = device;
+    h->gain = gain;
+
+    // tables: tw4096 | post8192 | hsel[0..6]
+    size_t nsel = 0;
+    for (int d = 0; d < SDDC_DDC_NDEC; d++) nsel += (size_t)(SDDC_DDC_HALF_FFT >> d);
+    const size_t ntab = 2 * (size_t)SDDC_DDC_HALF_FFT + nsel;
+    std::vector<float2> host(ntab);
+    for (int k = 0; k < SDDC_DDC_HALF_FFT; k++) {
+        const double a = -2.0 * M_PI * (double)k / 4096.0;
+        const double b = -2.0 * M_PI * (double)k / 8192.0;
+        host[k] = make_float2((float)std::cos(a), (float)std::sin(a));
+        host[SDDC_DDC_HALF_FFT + k] = make_float2((float)std::cos(b), (float)std::sin(b));
+    }
+    size_t off = 2 * (size_t)SDDC_DDC_HALF_FFT;
+    size_t sel_off[SDDC_DDC_NDEC];
+    std::vector<std::complex<double>> H(SDDC_DDC_HALF_FFT);
+    for (int d = 0; d < SDDC_DDC_NDEC; d++) {
+        sddc::filter_response(gain, d, H.data());
+        const int mfft = SDDC_DDC_HALF_FFT >> d;
+        sel_off[d] = off;
+        for (int m = 0; m < mfft; m++) {
+            // inverse-input position m: H[m] (m < mfft/2), H[4096 - mfft + m] otherwise
+            // (impl.hpp:90,94 with filter2 = filter + halfFft - mfft/2, impl.hpp:7)
+            const std::complex<double> v = H[m < mfft / 2 ? m : SDDC_DDC_HALF_FFT - mfft + m];
+            host[off + m] = make_float2((float)(0.5 * v.real()), (float)(0.5 * v.imag()));
+        }
+        off += (size_t)mfft;
+    }
+    hipError_t e = hipMalloc(&h->d_tables, ntab * sizeof(float2));
+    if (e == hipSuccess) e = hipMemcpy(h->d_tables, host.data(), ntab * sizeof(float2), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        sddc_ddc_destroy(h);
+        return fail(SDDC_ERR_HIP, "create: %s", hipGetErrorString(e));
+    }
+    h->tables.tw4096 = h->d_tables;
+    h->tables.post8192 = h->d_tables + SDDC_DDC_HALF_FFT;
+    for (int d = 0; d < SDDC_DDC_NDEC; d++) h->tables.hsel[d] = h->d_tables + sel_off[d];
+    *out = h;
+    return SDDC_OK;
+}
+
+int sddc_ddc_destroy(sddc_ddc_t *h)
+{
+    if (!h) return SDDC_OK;
+    {
+        DeviceGuard g(h->device);
+        if (h->stream) (void)hipStreamSynchronize(h->stream);
+        if (h->d_tables) (void)hipFree(h->d_tables);
+        if (h->d_in) (void)hipFree(h->d_in);
+        if (h->d_out) (void)hipFree(h->d_out);
+        if (h->d_tunebins) (void)hipFree(h->d_tunebins);
+        if (h->h_in) (void)hipHostFree(h->h_in);
+        if (h->h_out) (void)hipHostFree(h->h_out);
+        if (h->stream) (void)hipStreamDestroy(h->stream);
+    }
+    delete h;
+    return SDDC_OK;
+}
+
+int sddc_ddc_set_decimation(sddc_ddc_t *h, int d)
+{
+    if (!h) return fail(SDDC_ERR_ARG, "null handle");
+    if (d < 0 || d >= SDDC_DDC_NDEC) return fail(SDDC_ERR_ARG, "decimation index %d outside 0..6", d);
+    h->d = d;
+    return SDDC_OK;
+}
+
+int sddc_ddc_set_sideband(sddc_ddc_t *h, int lsb)
+{
+    if (!h) return fail(SDDC_ERR_ARG, "null handle");
+    h->lsb = lsb ? 1 : 0;
+    return SDDC_OK;
+}
+
+int sddc_ddc_set_rand(sddc_ddc_t *h, int rand)
+{
+    if (!h) return fail(SDDC_ERR_ARG, "null handle");
+    h->rand = rand ? 1 : 0;
+    return SDDC_OK;
+}
+
+int sddc_ddc_set_tunebin(sddc_ddc_t *h, int tunebin)
+{
+    if (!h) return fail(SDDC_ERR_ARG, "null handle");
+    if (tunebin < 0 || tunebin >= SDDC_DDC_HALF_FFT)
+        return fail(SDDC_ERR_ARG, "tune bin %d outside [0,4096)", tunebin);
+    h->tunebin = tunebin;
+    return SDDC_OK;
+}
+
+int sddc_ddc_get_tunebin(const sddc_ddc_t *h) { return h ? h->tunebin : -1; }
+
+float sddc_ddc_set_freq_offset(sddc_ddc_t *h, float offset)
+{
+    if (!h) {
+        fail(SDDC_ERR_ARG, "null handle");
+        return 0.f;
+    }
+    // fft_mt_r2iq.cpp:104-106
+    int tb = (int)(offset * SDDC_DDC_HALF_FFT / 4) * 4;
+    const float delta = ((float)tb / SDDC_DDC_HALF_FFT) - offset;
+    const float ret = delta * (float)(1 << h->d);
+    tb = std::min(std::max(tb, 0), SDDC_DDC_HALF_FFT - 4);
+    h->tunebin = tb;
+    return ret;
+}
+
+int sddc_ddc_reset(sddc_ddc_t *h)
+{
+    if (!h) return fail(SDDC_ERR_ARG, "null handle");
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (h->h_in) std::memset(h->h_in, 0, kHistory * sizeof(int16_t));
+    return SDDC_OK;
+}
+
+static int check_process_args(sddc_ddc_t *h, const int16_t *in, int nblk, const void *out)
+{
+    if (!h) return fail(SDDC_ERR_ARG, "null handle");
+    if (nblk <= 0) return fail(SDDC_ERR_ARG, "nblk must be > 0 (got %d)", nblk);
+    if (!in || !out) return fail(SDDC_ERR_ARG, "null buffer");
+    if (((uintptr_t)in & 3) != 0) return fail(SDDC_ERR_ARG, "input must be 4-byte aligned");
+    if (((uintptr_t)out & 7) != 0) return fail(SDDC_ERR_ARG, "output must be 8-byte aligned");
+    return SDDC_OK;
+}
+
+int sddc_ddc_process_device(sddc_ddc_t *h, const int16_t *d_in, int nblk, float *d_out, void *hip_stream)
+{
+    int rc = check_process_args(h, d_in, nblk, d_out);
+    if (rc) return rc;
+    DeviceGuard g(h->device);
+    HIP_TRY(g.err);
+    HIP_TRY(sddc::launch_frames(h->tables, h->d, d_in, nblk, d_out, h->tunebin, h->lsb, h->rand,
+                                (hipStream_t)hip_stream));
+    return SDDC_OK;
+}
+
+int sddc_ddc_process_channels_device(sddc_ddc_t *h, const int16_t *d_in, int nblk, const int *tunebins,
+                                     int nch, float *d_out, size_t out_stride_floats, void *hip_stream)
+{
+    int rc = check_process_args(h, d_in, nblk, d_out);
+    if (rc) return rc;
+    if (!tunebins || nch <= 0 || nch > SDDC_DDC_MAX_CHANNELS)
+        return fail(SDDC_ERR_ARG, "channel count %d outside 1..%d", nch, SDDC_DDC_MAX_CHANNELS);
+    for (int c = 0; c < nch; c++)
+        if (tunebins[c] < 0 || tunebins[c] >= SDDC_DDC_HALF_FFT)
+            return fail(SDDC_ERR_ARG, "channel %d tune bin %d outside [0,4096)", c, tunebins[c]);
+    const size_t need = (size_t)nblk * (size_t)(SDDC_DDC_OUT_BLOCK >> h->d) * 2;
+    if (nch > 1 && out_stride_floats < need)
+        return fail(SDDC_ERR_ARG, "out_stride_floats %zu < %zu floats per channel", out_stride_floats, need);
+    DeviceGuard g(h->device);
+    HIP_TRY(g.err);
+    std::lock_guard<std::mutex> lk(h->mu);
+    hipStream_t s = (hipStream_t)hip_stream;
+    if (h->tunebins_cached.size() != (size_t)nch ||
+        !std::equal(h->tunebins_cached.begin(), h->tunebins_cached.end(), tunebins)) {
+        if (!h->d_tunebins) HIP_TRY(hipMalloc(&h->d_tunebins, SDDC_DDC_MAX_CHANNELS * sizeof(int)));
+        h->tunebins_cached.assign(tunebins, tunebins + nch);
+        // synchronous: the host array may go away after we return
+        HIP_TRY(hipMemcpy(h->d_tunebins, tunebins, nch * sizeof(int), hipMemcpyHostToDevice));
+    }
+    HIP_TRY(sddc::launch_channels(h->tables, h->d, d_in, nblk, h->d_tunebins, nch, d_out,
+                                  out_stride_floats, h->lsb, h->rand, s));
+    return SDDC_OK;
+}
+
+int sddc_ddc_process_host(sddc_ddc_t *h, const int16_t *in, int nblk, float *out)
+{
+    int rc = check_process_args(h, in, nblk, out);
+    if (rc) return rc;
+    DeviceGuard g(h->device);
+    HIP_TRY(g.err);
+    std::lock_guard<std::mutex> lk(h->mu);
+    const size_t in_elems = kHistory + (size_t)kHostChunk * kBlock;
+    const size_t out_floats = (size_t)kHostChunk * SDDC_DDC_OUT_BLOCK * 2;
+    if (!h->h_in) {
+        HIP_TRY(hipHostMalloc(&h->h_in, in_elems * sizeof(int16_t), hipHostMallocDefault));
+        std::memset(h->h_in, 0, kHistory * sizeof(int16_t));
+        HIP_TRY(hipHostMalloc(&h->h_out, out_floats * sizeof(float), hipHostMallocDefault));
+        HIP_TRY(hipMalloc(&h->d_in, in_elems * sizeof(int16_t)));
+        HIP_TRY(hipMalloc(&h->d_out, out_floats * sizeof(float)));
+    }
+    const int per_blk_out = (SDDC_DDC_OUT_BLOCK >> h->d) * 2;
+    for (int done = 0; done < nblk;) {
+        const int n = std::min(kHostChunk, nblk - done);
+        const size_t nin = kHistory + (size_t)n * kBlock;
+        std::memcpy(h->h_in + kHistory, in + (size_t)done * kBlock, (size_t)n * kBlock * sizeof(int16_t));
+        HIP_TRY(hipMemcpyAsync(h->d_in, h->h_in, nin * sizeof(int16_t), hipMemcpyHostToDevice, h->stream));
+        HIP_TRY(sddc::launch_frames(h->tables, h->d, h->d_in, n, h->d_out, h->tunebin, h->lsb, h->rand,
+                                    h->stream));
+        HIP_TRY(hipMemcpyAsync(h->h_out, h->d_out, (size_t)n * per_blk_out * sizeof(float),
+                               hipMemcpyDeviceToHost, h->stream));
+        HIP_TRY(hipStreamSynchronize(h->stream));
+        std::memcpy(out + (size_t)done * per_blk_out, h->h_out, (size_t)n * per_blk_out * sizeof(float));
+        // keep the last 4096 samples as the next history (impl.hpp:32)
+        std::memmove(h->h_in, h->h_in + (size_t)n * kBlock, kHistory * sizeof(int16_t));
+        done += n;
+    }
+    return SDDC_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,206 @@
+// fft_device.hpp — register-level DFT cores and the LDS Stockham pass used by the
+// fused r2iq kernels (ddc_kernels.hip).  gfx950 / wave64; one workgroup of NT
+// threads owns one FFT in LDS.
+//
+// Conventions: unnormalised DFT, DIR = -1 forward (FFTW_FORWARD, e^{-2 pi i nk/N}),
+// DIR = +1 backward (FFTW_BACKWARD) — the sign conventions of the reference's
+// fftwf_plan_dft_r2c_1d / fftwf_plan_dft_1d(..., FFTW_BACKWARD) calls
+// (Core/fft_mt_r2iq.cpp:221-225).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+namespace sddc {
+
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ float2 cmul(float2 a, float2 b)
+{
+    return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+// a * conj(b)
+__device__ __forceinline__ float2 cmulc(float2 a, float2 b)
+{
+    return make_float2(a.x * b.x + a.y * b.y, a.y * b.x - a.x * b.y);
+}
+// a * (DIR * i)
+template <int DIR>
+__device__ __forceinline__ float2 mulj(float2 a)
+{
+    return DIR < 0 ? make_float2(a.y, -a.x) : make_float2(-a.y, a.x);
+}
+
+// cos/sin(2*pi*m/16), exact-to-float constants
+constexpr float kC16_1 = 0.92387953251128675613f;  // cos(pi/8)
+constexpr float kS16_1 = 0.38268343236508977173f;  // sin(pi/8)
+constexpr float kR2 = 0.70710678118654752440f;     // cos(pi/4)
+
+// a * e^{DIR*2*pi*i*m/16} for a compile-time m (0 <= m < 16)
+template <int DIR, int M>
+__device__ __forceinline__ float2 tw16(float2 a)
+{
+    constexpr int m = M & 15;
+    if constexpr (m == 0) return a;
+    else if constexpr (m == 4) return mulj<DIR>(a);
+    else if constexpr (m == 8) return make_float2(-a.x, -a.y);
+    else if constexpr (m == 12) return mulj<-DIR>(a);
+    else if constexpr (m == 2 || m == 6 || m == 10 || m == 14) {
+        // e^{DIR i pi/4 * (m/2)}: (+-r2, +-r2)
+        constexpr float c = (m == 2 || m == 14) ? kR2 : -kR2;
+        constexpr float s = (m == 2 || m == 6) ? kR2 : -kR2;
+        constexpr float sd = DIR * s;
+        return make_float2(c * a.x - sd * a.y, c * a.y + sd * a.x);
+    } else {
+        // odd m: cos/sin of multiples of pi/8
+        constexpr float c = (m == 1 || m == 15) ? kC16_1 : (m == 3 || m == 13) ? kS16_1
+                          : (m == 5 || m == 11) ? -kS16_1 : -kC16_1;
+        constexpr float s = (m == 1 || m == 7) ? kS16_1 : (m == 3 || m == 5) ? kC16_1
+                          : (m == 9 || m == 15) ? -kS16_1 : -kC16_1;
+        constexpr float sd = DIR * s;
+        return make_float2(c * a.x - sd * a.y, c * a.y + sd * a.x);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// In-register DFTs, natural order in -> natural order out (o may alias nothing).
+// ---------------------------------------------------------------------------
+template <int DIR>
+__device__ __forceinline__ void dft2(const float2 *v, float2 *o)
+{
+    o[0] = cadd(v[0], v[1]);
+    o[1] = csub(v[0], v[1]);
+}
+
+template <int DIR>
+__device__ __forceinline__ void dft4(float2 a0, float2 a1, float2 a2, float2 a3,
+                                     float2 &o0, float2 &o1, float2 &o2, float2 &o3)
+{
+    const float2 t0 = cadd(a0, a2), t1 = csub(a0, a2);
+    const float2 t2 = cadd(a1, a3), t3 = mulj<DIR>(csub(a1, a3));
+    o0 = cadd(t0, t2);
+    o2 = csub(t0, t2);
+    o1 = cadd(t1, t3);
+    o3 = csub(t1, t3);
+}
+
+template <int DIR>
+__device__ __forceinline__ void dft4(const float2 *v, float2 *o)
+{
+    dft4<DIR>(v[0], v[1], v[2], v[3], o[0], o[1], o[2], o[3]);
+}
+
+// 8 = 4 x 2: n = 2 n1 + n2, k = k1 + 4 k2
+template <int DIR>
+__device__ __forceinline__ void dft8(const float2 *v, float2 *o)
+{
+    float2 b0[4], b1[4];
+    dft4<DIR>(v[0], v[2], v[4], v[6], b0[0], b0[1], b0[2], b0[3]);
+    dft4<DIR>(v[1], v[3], v[5], v[7], b1[0], b1[1], b1[2], b1[3]);
+    b1[1] = tw16<DIR, 2>(b1[1]);
+    b1[2] = tw16<DIR, 4>(b1[2]);
+    b1[3] = tw16<DIR, 6>(b1[3]);
+#pragma unroll
+    for (int k1 = 0; k1 < 4; k1++) {
+        o[k1] = cadd(b0[k1], b1[k1]);
+        o[k1 + 4] = csub(b0[k1], b1[k1]);
+    }
+}
+
+// 16 = 4 x 4: n = 4 n1 + n2, k = k1 + 4 k2
+template <int DIR>
+__device__ __forceinline__ void dft16(const float2 *v, float2 *o)
+{
+    float2 b[4][4];  // b[n2][k1]
+#pragma unroll
+    for (int n2 = 0; n2 < 4; n2++)
+        dft4<DIR>(v[n2], v[4 + n2], v[8 + n2], v[12 + n2], b[n2][0], b[n2][1], b[n2][2], b[n2][3]);
+    b[1][1] = tw16<DIR, 1>(b[1][1]);
+    b[1][2] = tw16<DIR, 2>(b[1][2]);
+    b[1][3] = tw16<DIR, 3>(b[1][3]);
+    b[2][1] = tw16<DIR, 2>(b[2][1]);
+    b[2][2] = tw16<DIR, 4>(b[2][2]);
+    b[2][3] = tw16<DIR, 6>(b[2][3]);
+    b[3][1] = tw16<DIR, 3>(b[3][1]);
+    b[3][2] = tw16<DIR, 6>(b[3][2]);
+    b[3][3] = tw16<DIR, 9>(b[3][3]);
+#pragma unroll
+    for (int k1 = 0; k1 < 4; k1++)
+        dft4<DIR>(b[0][k1], b[1][k1], b[2][k1], b[3][k1], o[k1], o[k1 + 4], o[k1 + 8], o[k1 + 12]);
+}
+
+template <int R, int DIR>
+__device__ __forceinline__ void dft(const float2 *v, float2 *o)
+{
+    if constexpr (R == 2) dft2<DIR>(v, o);
+    else if constexpr (R == 4) dft4<DIR>(v, o);
+    else if constexpr (R == 8) dft8<DIR>(v, o);
+    else {
+        static_assert(R == 16, "radix must be 2, 4, 8 or 16");
+        dft16<DIR>(v, o);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// LDS layout: complex element i lives at float2 slot lds_pad(i) = i + i/16.
+// One pad slot per 16 elements keeps the radix-16 "16 consecutive per lane"
+// writes of the first pass conflict-free on ds_write_b64 (bank = dword/2 mod 32).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int lds_pad(int i) { return i + (i >> 4); }
+constexpr int lds_slots(int n) { return n + n / 16; }
+
+// ---------------------------------------------------------------------------
+// One Stockham radix-R pass of an N-point transform (DIT, autosort), NT threads.
+//   in  position for butterfly j, leg r:  j + r*N/R
+//   out position:                          (j/NS)*NS*R + j%NS + r*NS
+//   twiddle of leg r:  W_{NS*R}^{(j%NS)*r}, read from tw4096[k] = e^{-2 pi i k/4096}
+//                      (conjugated for DIR = +1).  N*... must divide 4096.
+// `load(pos)` supplies inputs, `store(pos, value)` consumes outputs.  The caller
+// places the barriers: a pass reads everything into registers, then the caller
+// syncs, then the pass stores (so one LDS buffer serves in and out).
+// ---------------------------------------------------------------------------
+template <int N, int R, int NS, int NT>
+struct StockhamPass {
+    static constexpr int NB = N / R;                 // butterflies
+    static constexpr int PER = (NB + NT - 1) / NT;   // butterflies per thread
+    static_assert(N % R == 0 && 4096 % (NS * R) == 0, "bad pass geometry");
+    float2 v[PER][R];
+
+    template <int DIR, class Load>
+    __device__ __forceinline__ void compute(Load load, const float2 *__restrict__ tw4096)
+    {
+#pragma unroll
+        for (int i = 0; i < PER; i++) {
+            const int j = (int)threadIdx.x + i * NT;
+            if (NB % NT == 0 || j < NB) {
+                float2 a[R];
+#pragma unroll
+                for (int r = 0; r < R; r++) a[r] = load(j + r * NB);
+                if constexpr (NS > 1) {
+                    const int step = (j % NS) * (4096 / (NS * R));
+#pragma unroll
+                    for (int r = 1; r < R; r++) {
+                        const float2 w = tw4096[step * r];
+                        a[r] = DIR < 0 ? cmul(a[r], w) : cmulc(a[r], w);
+                    }
+                }
+                dft<R, DIR>(a, v[i]);
+            }
+        }
+    }
+
+    template <class Store>
+    __device__ __forceinline__ void store(Store st) const
+    {
+#pragma unroll
+        for (int i = 0; i < PER; i++) {
+            const int j = (int)threadIdx.x + i * NT;
+            if (NB % NT == 0 || j < NB) {
+                const int base = (j / NS) * NS * R + (j % NS);
+#pragma unroll
+                for (int r = 0; r < R; r++) st(base + r * NS, v[i][r]);
+            }
+        }
+    }
+};
+
+}  // namespace sddc

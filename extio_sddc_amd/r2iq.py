@@ -1,0 +1,185 @@
+"""Host-side mirror of the reference's r2iq operator interface over the C ABI.
+
+``R2iq`` exposes the method names and argument meanings of
+``r2iqControlClass`` / ``fft_mt_r2iq`` (Core/r2iq.h:16-48,
+Core/fft_mt_r2iq.h:21-31) so the parity tests read like the reference's own
+tests; the work is done by the gfx950 kernels behind include/sddc_ddc.h.
+
+Reference interface              -> here
+  Init(gain, in, out)  .cpp:147  -> R2iq(gain, device)
+  setDecimate(d)       r2iq.h:31 -> setDecimate(d)
+  updateRand(v)        r2iq.h:25 -> updateRand(v) / getRand()
+  setSideband(lsb)     r2iq.h:28 -> setSideband(lsb) / getSideband()
+  getRatio()           r2iq.h:21 -> getRatio()
+  setFreqOffset(off)   .cpp:101  -> setFreqOffset(off) -> fine-tune residual
+  TurnOn()             .cpp:111  -> TurnOn()  (stream reset: zero history)
+  worker body  impl.hpp:15-152   -> process(blocks) (host) / process_device(...) (HBM)
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import DDCError, check
+
+HALF_FFT = 4096        # fft_mt_r2iq.h:18
+BLOCK = 65536          # config.h:80-81 transferSamples
+FRAMES = 11            # fft_mt_r2iq.h:19 fftPerBuf
+NDEC = 7               # r2iq.h:5 NDECIDX
+OUT_BLOCK = 32768      # config.h:62 EXT_BLOCKLEN
+NTAPS = 1025
+BBRF103_GAINFACTOR = 7.8e-8   # config.h:57; DummyRadio's gain in the reference tests
+
+
+def output_samples(d: int, nblk: int) -> int:
+    return nblk * (OUT_BLOCK >> d)
+
+
+def kaiser(ntaps: int, astop: float, fpass: float, fstop: float):
+    """KaiserWindow (Core/fir.cpp:48-105); ntaps <= 0 returns the tap estimate."""
+    L = _lib.load()
+    if ntaps <= 0:
+        return L.sddc_ddc_kaiser(ntaps, astop, fpass, fstop, None)
+    out = np.zeros(ntaps, np.float32)
+    n = L.sddc_ddc_kaiser(ntaps, astop, fpass, fstop, out.ctypes.data)
+    return out[:n]
+
+
+def filter_taps(d: int) -> np.ndarray:
+    out = np.zeros(NTAPS, np.float32)
+    check(_lib.load().sddc_ddc_filter_taps(d, out.ctypes.data))
+    return out
+
+
+def filter_response(gain: float, d: int) -> np.ndarray:
+    out = np.zeros((HALF_FFT, 2), np.float32)
+    check(_lib.load().sddc_ddc_filter_response(gain, d, out.ctypes.data))
+    return out[:, 0] + 1j * out[:, 1]
+
+
+def device_count() -> int:
+    return _lib.load().sddc_ddc_device_count()
+
+
+class R2iq:
+    """The DDC for one stream on one GPU (one handle = one r2iq worker)."""
+
+    def __init__(self, gain: float = 1.0, device: int = 0):
+        self._L = _lib.load()
+        h = ctypes.c_void_p()
+        check(self._L.sddc_ddc_create(gain, device, ctypes.byref(h)))
+        self._h = h
+        self.gain = gain
+        self.device = device
+        self._d = 0
+        self._rand = False
+        self._lsb = False
+
+    # -- lifecycle --------------------------------------------------------
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self._L.sddc_ddc_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # -- r2iqControlClass -------------------------------------------------
+    def setDecimate(self, d: int) -> None:
+        check(self._L.sddc_ddc_set_decimation(self._h, d))
+        self._d = d
+
+    def getDecimate(self) -> int:
+        return self._d
+
+    def getRatio(self) -> int:
+        return 1 << self._d          # mratio[mdecimation], fft_mt_r2iq.cpp:32-36
+
+    def updateRand(self, v: bool) -> None:
+        check(self._L.sddc_ddc_set_rand(self._h, int(bool(v))))
+        self._rand = bool(v)
+
+    def getRand(self) -> bool:
+        return self._rand
+
+    def setSideband(self, lsb: bool) -> None:
+        check(self._L.sddc_ddc_set_sideband(self._h, int(bool(lsb))))
+        self._lsb = bool(lsb)
+
+    def getSideband(self) -> bool:
+        return self._lsb
+
+    def setFreqOffset(self, offset: float) -> float:
+        return float(self._L.sddc_ddc_set_freq_offset(self._h, offset))
+
+    def setTuneBin(self, tunebin: int) -> None:
+        check(self._L.sddc_ddc_set_tunebin(self._h, tunebin))
+
+    def getTuneBin(self) -> int:
+        return self._L.sddc_ddc_get_tunebin(self._h)
+
+    def TurnOn(self) -> None:
+        check(self._L.sddc_ddc_reset(self._h))
+
+    # -- the hot loop -----------------------------------------------------
+    def process(self, blocks: np.ndarray) -> np.ndarray:
+        """Stateful host path: nblk blocks (int16) -> nblk*(32768>>d) complex64."""
+        blocks = np.ascontiguousarray(blocks, np.int16).reshape(-1)
+        if blocks.size % BLOCK:
+            raise DDCError(-1, f"input length {blocks.size} is not a multiple of {BLOCK}")
+        nblk = blocks.size // BLOCK
+        out = np.empty((output_samples(self._d, nblk), 2), np.float32)
+        check(self._L.sddc_ddc_process_host(self._h, blocks.ctypes.data, nblk, out.ctypes.data))
+        return out.view(np.complex64).reshape(-1)
+
+    def process_device(self, d_in, nblk: int, d_out, stream=None) -> None:
+        """Stateless HBM path.  d_in: int16 device tensor [4096 + nblk*65536];
+        d_out: float32 device tensor [>= nblk*(32768>>d)*2].  Enqueued on `stream`
+        (a torch.cuda.Stream or raw handle; default: torch's current stream)."""
+        _check_device_buffers(d_in, nblk, d_out, output_samples(self._d, nblk) * 2)
+        check(self._L.sddc_ddc_process_device(self._h, d_in.data_ptr(), nblk, d_out.data_ptr(),
+                                              _stream_handle(stream)))
+
+    def process_channels_device(self, d_in, nblk: int, tunebins, d_out, stream=None) -> None:
+        """Many-channel path: d_out float32 [nch, nblk*(32768>>d)*2]."""
+        tb = np.ascontiguousarray(np.asarray(tunebins, np.int32))
+        nch = tb.size
+        per = output_samples(self._d, nblk) * 2
+        _check_device_buffers(d_in, nblk, d_out, per * nch)
+        stride = d_out.stride(0) if d_out.dim() > 1 else per
+        check(self._L.sddc_ddc_process_channels_device(self._h, d_in.data_ptr(), nblk, tb.ctypes.data, nch,
+                                                       d_out.data_ptr(), stride, _stream_handle(stream)))
+
+
+def _check_device_buffers(d_in, nblk, d_out, out_floats):
+    import torch
+    if not (d_in.is_cuda and d_out.is_cuda):
+        raise DDCError(-1, "device path needs device tensors")
+    if d_in.dtype != torch.int16 or d_out.dtype != torch.float32:
+        raise DDCError(-1, "d_in must be int16 and d_out float32")
+    if not (d_in.is_contiguous() and d_out.is_contiguous()):
+        raise DDCError(-1, "tensors must be contiguous")
+    if d_in.numel() < HALF_FFT + nblk * BLOCK:
+        raise DDCError(-1, f"d_in has {d_in.numel()} samples, need {HALF_FFT + nblk * BLOCK}")
+    if d_out.numel() < out_floats:
+        raise DDCError(-1, f"d_out has {d_out.numel()} floats, need {out_floats}")
+
+
+def _stream_handle(stream):
+    if stream is None:
+        import torch
+        return torch.cuda.current_stream().cuda_stream
+    if isinstance(stream, int):
+        return stream
+    return stream.cuda_stream

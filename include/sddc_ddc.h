@@ -1,0 +1,128 @@
+/*
+ * sddc_ddc.h — C ABI of the MI355X-native real-to-IQ down-converter.
+ *
+ * This is the thin C boundary UNDER the drop-in C++ class `fft_mt_r2iq`
+ * (include/fft_mt_r2iq.h), which keeps the reference's r2iqControlClass
+ * interface (Core/r2iq.h:16-48) so RadioHandler / libsddc / ExtIO / SoapySDDC
+ * load it unchanged.  Plain pointers and sizes only; no C++ or torch types.
+ * Every entry point names the reference interface it replaces (file:line,
+ * relative to the ExtIO_sddc tree).
+ *
+ * Conventions (pinned to the reference):
+ *   block      = 65536 int16 real ADC samples           (config.h:80-81 transferSamples)
+ *   history    = the 4096 samples preceding a block      (fft_mt_r2iq_impl.hpp:32)
+ *   d          = decimation index 0..6, mfft = 4096>>d   (r2iq.h:5,39; fft_mt_r2iq.cpp:44-48)
+ *   output     = 8*mfft = 32768>>d complex float32 (I,Q interleaved) per input block
+ *                (fft_mt_r2iq_impl.hpp:117-138); 2^d blocks fill one 32768-sample
+ *                EXT_BLOCKLEN output block (config.h:62)
+ *   tunebin    = forward-FFT bin moved to DC, multiple of 4 in [0,4096)
+ *                (fft_mt_r2iq.cpp:101-109)
+ *
+ * Errors: every int-returning call returns SDDC_OK (0) or a negative SDDC_ERR_*;
+ * sddc_ddc_last_error() gives a thread-local message.  Nothing throws across this
+ * boundary (the reference's r2iq methods are void/bool/float).
+ * There is no CPU fallback: without a usable gfx950 device sddc_ddc_create()
+ * fails with SDDC_ERR_NODEV.
+ */
+#ifndef SDDC_DDC_H
+#define SDDC_DDC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SDDC_DDC_ABI_VERSION 1
+
+#define SDDC_DDC_HALF_FFT   4096    /* halfFft               fft_mt_r2iq.h:18 */
+#define SDDC_DDC_FFTN       8192    /* FFTN_R_ADC            config.h:49 */
+#define SDDC_DDC_HOP        6144    /* 3*halfFft/2           fft_mt_r2iq_impl.hpp:88 */
+#define SDDC_DDC_BLOCK      65536   /* transferSamples       config.h:80-81 */
+#define SDDC_DDC_FRAMES     11      /* fftPerBuf             fft_mt_r2iq.h:19 */
+#define SDDC_DDC_NDEC       7       /* NDECIDX               r2iq.h:5 */
+#define SDDC_DDC_NTAPS      1025    /* halfFft/4+1 taps      fft_mt_r2iq.cpp:181 */
+#define SDDC_DDC_OUT_BLOCK  32768   /* EXT_BLOCKLEN          config.h:62 */
+#define SDDC_DDC_MAX_CHANNELS 1024  /* 1024 legal tune bins (tunebin = 4c) */
+
+enum {
+    SDDC_OK = 0,
+    SDDC_ERR_ARG = -1,     /* bad argument (range, null, alignment)           */
+    SDDC_ERR_HIP = -2,     /* a HIP runtime call or kernel launch failed       */
+    SDDC_ERR_NODEV = -3,   /* no usable gfx950 device                          */
+    SDDC_ERR_STATE = -4,   /* call not valid in the handle's current state     */
+    SDDC_ERR_NOMEM = -5    /* host or device allocation failed                 */
+};
+
+typedef struct sddc_ddc sddc_ddc_t;
+
+/* ---- library ------------------------------------------------------------ */
+int         sddc_ddc_abi_version(void);
+const char *sddc_ddc_last_error(void);
+/* Number of visible HIP devices (0 if none / runtime unusable). */
+int         sddc_ddc_device_count(void);
+
+/* ---- filter design (host; Core/fir.cpp, fft_mt_r2iq.cpp:163-208) ---------- */
+/* KaiserWindow(num_taps, Astop, normFpass, normFstop, Coef)   fir.cpp:48-105.
+ * Bit-identical float arithmetic.  coef == NULL with ntaps <= 0 returns the
+ * tap-count estimate, exactly like the reference. */
+int sddc_ddc_kaiser(int ntaps, float astop, float fpass, float fstop, float *coef);
+/* The 1025 taps for decimation index d (fft_mt_r2iq.cpp:189-191). */
+int sddc_ddc_filter_taps(int d, float *taps /* [1025] */);
+/* H_d = FFT4096(time-reversed gain*2048/8192*taps)  (fft_mt_r2iq.cpp:193-205),
+ * evaluated in double and rounded once to float. */
+int sddc_ddc_filter_response(float gain, int d, float *H /* [4096][2] */);
+
+/* ---- lifecycle: fft_mt_r2iq::Init (fft_mt_r2iq.cpp:147-227), dtor (:71-98) - */
+/* Builds the 7 filter banks for `gain` (hardware->getGain(), RadioHandler.cpp:142)
+ * and uploads them with the FFT twiddle tables to `device`. */
+int sddc_ddc_create(float gain, int device, sddc_ddc_t **out);
+int sddc_ddc_destroy(sddc_ddc_t *h);
+
+/* ---- control: r2iqControlClass (r2iq.h:23-31) and fft_mt_r2iq -------------- */
+int   sddc_ddc_set_decimation(sddc_ddc_t *h, int d);        /* setDecimate   r2iq.h:31 */
+int   sddc_ddc_set_sideband(sddc_ddc_t *h, int lsb);        /* setSideband   r2iq.h:28 */
+int   sddc_ddc_set_rand(sddc_ddc_t *h, int rand);           /* updateRand    r2iq.h:25 */
+int   sddc_ddc_set_tunebin(sddc_ddc_t *h, int tunebin);     /* mtunebin      fft_mt_r2iq.h:97 */
+int   sddc_ddc_get_tunebin(const sddc_ddc_t *h);
+/* setFreqOffset(offset)  fft_mt_r2iq.cpp:101-109: tunebin = int(offset*1024)*4,
+ * returns the fine-tune residual (tunebin/4096 - offset) * 2^d.  Valid domain
+ * 0 <= offset < 1 (fraction of Fs/2); outside it the tune bin is clamped into
+ * [0, 4092] (the reference would read out of range, impl.hpp:76-79). */
+float sddc_ddc_set_freq_offset(sddc_ddc_t *h, float offset);
+/* TurnOn() stream reset (fft_mt_r2iq.cpp:111-129): zero history, seq = 0. */
+int   sddc_ddc_reset(sddc_ddc_t *h);
+
+/* Complex samples produced per nblk input blocks at decimation d: nblk*(32768>>d). */
+size_t sddc_ddc_output_samples(int d, int nblk);
+
+/* ---- the hot loop (fft_mt_r2iq_impl.hpp:15-152) ---------------------------- */
+/* Stateless, device-resident.  d_in: device int16 [4096 + nblk*65536] = the
+ * 4096-sample history followed by nblk blocks (2-byte aligned; 4-byte aligned
+ * start required).  d_out: device float [nblk*(32768>>d)*2], (I,Q) pairs, in
+ * stream order.  Uses the handle's d / sideband / rand / tunebin.  Enqueued on
+ * `hip_stream` (a hipStream_t; NULL = default stream); returns after launch. */
+int sddc_ddc_process_device(sddc_ddc_t *h, const int16_t *d_in, int nblk,
+                            float *d_out, void *hip_stream);
+
+/* Many-channel DDC: one forward transform per
+ * frame, shared by `nch` channels with their own tune bins (host array, each a
+ * multiple of 4 in [0,4096)).  d_out: channel c's stream starts at
+ * d_out + c*out_stride_floats.  All channels use the handle's d/sideband/rand. */
+int sddc_ddc_process_channels_device(sddc_ddc_t *h, const int16_t *d_in, int nblk,
+                                     const int *tunebins, int nch,
+                                     float *d_out, size_t out_stride_floats,
+                                     void *hip_stream);
+
+/* Stateful, host buffers: the r2iq worker body.  Consumes nblk consecutive
+ * blocks from `in` (host int16 [nblk*65536]), keeps the 4096-sample history
+ * across calls (zero after create/reset), writes nblk*(32768>>d) complex
+ * samples to `out` (host float, (I,Q) pairs).  Synchronous. */
+int sddc_ddc_process_host(sddc_ddc_t *h, const int16_t *in, int nblk, float *out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SDDC_DDC_H */
