@@ -8,15 +8,28 @@
 
 namespace sddc {
 
-// Device-resident constant tables, built once per handle (fft_mt_r2iq::Init).
+// Device-resident constant tables, built once per handle (the reference's
+// fft_mt_r2iq::Init builds filterHw and the FFTW plans, fft_mt_r2iq.cpp:147-227).
+// All twiddles are evaluated in double on the host and rounded once to float.
 struct KernelTables {
-    const float2 *tw4096 = nullptr;    // e^{-2 pi i k/4096}, k < 4096 (FFT twiddles)
-    const float2 *post8192 = nullptr;  // e^{-2 pi i k/8192}, k < 4096 (r2c split twiddles)
+    const float2 *tw4096 = nullptr;    // e^{-2 pi i k/4096}, k < 4096 (v1 FFT twiddles)
+    const float2 *post8192 = nullptr;  // e^{-2 pi i k/8192}, k < 8192 (r2c split twiddles)
     const float2 *hsel[7] = {};        // per d: mfft filter taps in inverse-input order, x 1/2
+    // persistent kernel (v2) twiddle sets
+    const float2 *tw_p1 = nullptr;     // [15][16]: W_256^{s r}     forward pass 1 (NS = 16)
+    const float2 *tw_q1[7] = {};       // [15][S]:  W_{16S}^{s r}   inverse pass 1, S = NS of that pass
+    const float2 *rec_f = nullptr;     // [2][256]: W_4096^{j}, W_4096^{4j}  forward pass 2 recurrence
+    const float2 *rec_i[7] = {};       // [2][256]: W_N^{j}, W_N^{4j}        inverse pass 2 (N >= 512)
 };
 
+// v1: one workgroup per frame (kept as a reference variant for A/B timing)
 hipError_t launch_frames(const KernelTables &t, int d, const int16_t *d_in, int nblk, float *d_out,
                          int tunebin, int lsb, int rand, hipStream_t s);
+
+// v2 (default): persistent workgroups, input prefetch, swizzled LDS
+hipError_t launch_frames_persistent(const KernelTables &t, int d, const int16_t *d_in, int nblk,
+                                    float *d_out, int tunebin, int lsb, int rand, int device,
+                                    hipStream_t s);
 
 int channels_per_group(int d, int nch);
 

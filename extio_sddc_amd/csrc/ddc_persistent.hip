@@ -1,0 +1,384 @@
+// ddc_persistent.hip — v2 single-channel r2iq kernel for gfx950: persistent workgroups.
+//
+// Same per-frame algorithm as ddc_kernels.hip (see its header for the mapping of
+// the reference's fft_mt_r2iq_impl.hpp:76-138 onto the passes), restructured for
+// throughput on MI355X:
+//   * persistent grid (CUs x resident workgroups); each workgroup walks a
+//     contiguous range of frames, so consecutive frames (which share 2048 input
+//     samples) stay on one CU / XCD L2;
+//   * the next frame's 16 int16 pairs per thread are loaded into registers while
+//     the current frame is transformed (hides the HBM latency the v1 kernel paid
+//     at every workgroup start);
+//   * LDS is addressed through an XOR swizzle e ^ ((e >> 4) & 15) instead of
+//     padding: 32 KB per frame, and both the 16-consecutive-per-lane writes of
+//     the first pass and the 64-consecutive reads are bank-conflict free;
+//   * twiddles: small [r][s] tables for the NS <= 16 passes (L1 resident), and a
+//     register recurrence from per-thread W^j, W^{4j} for the NS = 256 passes
+//     (no 30 KB L2 table stream per frame); the r2c split twiddle W_8192^bin is a
+//     per-thread base times a compile-time W_32 constant.
+#include <hip/hip_runtime.h>
+
+#include "ddc_kernels.h"
+#include "fft_device.hpp"
+
+namespace sddc {
+namespace {
+
+constexpr int NT = 256;
+constexpr int HALF = 4096;
+constexpr int HOP = 6144;
+constexpr int BLOCK = 65536;
+constexpr int FRAMES = 11;
+
+// W_32^q = e^{-2 pi i q/32}
+__device__ constexpr float kW32re[32] = {
+    1.0f, 9.807852804e-01f, 9.238795325e-01f, 8.314696123e-01f, 7.071067812e-01f, 5.555702330e-01f,
+    3.826834324e-01f, 1.950903220e-01f, 0.0f, -1.950903220e-01f, -3.826834324e-01f, -5.555702330e-01f,
+    -7.071067812e-01f, -8.314696123e-01f, -9.238795325e-01f, -9.807852804e-01f, -1.0f, -9.807852804e-01f,
+    -9.238795325e-01f, -8.314696123e-01f, -7.071067812e-01f, -5.555702330e-01f, -3.826834324e-01f,
+    -1.950903220e-01f, 0.0f, 1.950903220e-01f, 3.826834324e-01f, 5.555702330e-01f, 7.071067812e-01f,
+    8.314696123e-01f, 9.238795325e-01f, 9.807852804e-01f};
+__device__ constexpr float kW32im[32] = {
+    0.0f, -1.950903220e-01f, -3.826834324e-01f, -5.555702330e-01f, -7.071067812e-01f, -8.314696123e-01f,
+    -9.238795325e-01f, -9.807852804e-01f, -1.0f, -9.807852804e-01f, -9.238795325e-01f, -8.314696123e-01f,
+    -7.071067812e-01f, -5.555702330e-01f, -3.826834324e-01f, -1.950903220e-01f, 0.0f, 1.950903220e-01f,
+    3.826834324e-01f, 5.555702330e-01f, 7.071067812e-01f, 8.314696123e-01f, 9.238795325e-01f,
+    9.807852804e-01f, 1.0f, 9.807852804e-01f, 9.238795325e-01f, 8.314696123e-01f, 7.071067812e-01f,
+    5.555702330e-01f, 3.826834324e-01f, 1.950903220e-01f};
+
+__device__ __forceinline__ int swz(int e) { return e ^ ((e >> 4) & 15); }
+
+template <int DIR>
+__device__ __forceinline__ float2 tmul(float2 a, float2 w) { return DIR < 0 ? cmul(a, w) : cmulc(a, w); }
+
+__device__ __forceinline__ float derand(int v, int rand)
+{
+    // convert_float<rand>, Core/fft_mt_r2iq.h:36-51: odd samples XOR 0xFFFE when rand is on
+    return (float)(v ^ (-2 & -(v & rand & 1)));
+}
+
+// a[r] *= W^{r} for r = 1..15 given the forward-direction W^1 and W^4 of this lane
+// (conjugated for DIR = +1).  Every power is at most three products away.
+template <int DIR>
+__device__ __forceinline__ void twiddle_rec16(float2 *a, float2 w1, float2 w4)
+{
+    if (DIR > 0) {
+        w1.y = -w1.y;
+        w4.y = -w4.y;
+    }
+    const float2 w2 = cmul(w1, w1), w3 = cmul(w2, w1);
+    const float2 w8 = cmul(w4, w4), w12 = cmul(w8, w4);
+    a[1] = cmul(a[1], w1);
+    a[2] = cmul(a[2], w2);
+    a[3] = cmul(a[3], w3);
+    a[4] = cmul(a[4], w4);
+    a[5] = cmul(a[5], cmul(w4, w1));
+    a[6] = cmul(a[6], cmul(w4, w2));
+    a[7] = cmul(a[7], cmul(w4, w3));
+    a[8] = cmul(a[8], w8);
+    a[9] = cmul(a[9], cmul(w8, w1));
+    a[10] = cmul(a[10], cmul(w8, w2));
+    a[11] = cmul(a[11], cmul(w8, w3));
+    a[12] = cmul(a[12], w12);
+    a[13] = cmul(a[13], cmul(w12, w1));
+    a[14] = cmul(a[14], cmul(w12, w2));
+    a[15] = cmul(a[15], cmul(w12, w3));
+}
+
+// X[bin] * Hh[m] from Z in LDS (Hh = H/2): the r2c split E + W^bin O, times the filter.
+// Zero for bins the reference zero-fills (impl.hpp:91-92, 95-96).
+__device__ __forceinline__ float2 split_bin(const float2 *lds, int bin, float2 wbin, float2 hh)
+{
+    if (bin < 0 || bin >= HALF) return make_float2(0.f, 0.f);
+    const float2 zk = lds[swz(bin)];
+    const float2 zc = lds[swz((HALF - bin) & (HALF - 1))];
+    const float2 A = make_float2(zk.x + zc.x, zk.y - zc.y);
+    const float2 Bi = make_float2(zk.y + zc.y, zc.x - zk.x);   // (Zk - conj Zc) / i
+    return cmul(cadd(A, cmul(Bi, wbin)), hh);
+}
+
+template <int N>
+__device__ __forceinline__ void emit(float2 *__restrict__ out_blk, int k, int n, float2 v, float cs)
+{
+    v.y *= cs;
+    if (k == 0)
+        out_blk[n - N / 4] = v;
+    else
+        out_blk[N / 2 + (3 * N / 4) * (k - 1) + n] = v;
+}
+
+__device__ __forceinline__ void load_frame(const int *__restrict__ in32, int blk, int k, int (&x)[16])
+{
+    const int *p = in32 + ((size_t)blk * BLOCK + (size_t)k * HOP) / 2 + threadIdx.x;
+#pragma unroll
+    for (int r = 0; r < 16; r++) x[r] = p[NT * r];
+}
+
+template <int D>
+__global__ __launch_bounds__(NT, 2) void r2iq_persistent_kernel(
+    const int *__restrict__ in32, float2 *__restrict__ out, int nframes,
+    const float2 *__restrict__ tw_p1, const float2 *__restrict__ tw_q1,
+    const float2 *__restrict__ rec_f, const float2 *__restrict__ rec_i,
+    const float2 *__restrict__ post8192, const float2 *__restrict__ hsel,
+    int tunebin, int lsb, int rand)
+{
+    constexpr int N = HALF >> D;
+    __shared__ __attribute__((aligned(16))) float2 lds[HALF];
+
+    const int tid = (int)threadIdx.x;
+    const int G = (int)gridDim.x, w = (int)blockIdx.x;
+    const int f0 = (int)(((long long)nframes * w) / G);
+    const int f1 = (int)(((long long)nframes * (w + 1)) / G);
+    if (f0 >= f1) return;
+
+    // per-thread constants, live for the whole frame loop
+    const float2 fw1_ = rec_f[tid], fw4_ = rec_f[NT + tid];
+    float2 iw1_ = fw1_, iw4_ = fw4_;
+    if constexpr (N >= 512 && N < HALF) {
+        if (tid < N / 16) {
+            iw1_ = rec_i[tid];
+            iw4_ = rec_i[NT + tid];
+        }
+    }
+    const float2 pb_ = post8192[(tunebin + tid) & 8191];   // W_8192^{tb + tid}
+    const float cs = lsb ? -1.f : 1.f;
+
+    int blk = f0 / FRAMES, k = f0 - blk * FRAMES;
+    int x[16];
+    load_frame(in32, blk, k, x);
+
+    for (int f = f0; f < f1; f++) {
+        // Opaque per-iteration copies of the thread index and table pointers: without
+        // them the compiler hoists every loop-invariant LDS address and table load out
+        // of the frame loop and spills them.
+        int z = 0;
+        asm volatile("" : "+s"(z));
+        const int t = tid + z;
+        const float2 *tp1 = tw_p1 + z, *tq1 = tw_q1 + z, *hs = hsel + z, *pst = post8192 + z;
+        float2 fw1 = fw1_, fw4 = fw4_, iw1 = iw1_, iw4 = iw4_, pb = pb_;
+        asm volatile("" : "+v"(fw1), "+v"(fw4), "+v"(iw1), "+v"(iw4), "+v"(pb));
+        const int sT = swz(t);            // swz(t + 256 r) = sT + 256 r
+        const int x15 = t & 15;
+        float2 *out_blk = out + (size_t)blk * 8 * N;
+        const int kc = k;
+        // ---- forward pass 0 (R16, NS1): convert + DFT16 from registers ----
+        float2 v[16];
+        {
+            float2 a[16];
+#pragma unroll
+            for (int r = 0; r < 16; r++)
+                a[r] = make_float2(derand((int)(short)(x[r] & 0xffff), rand), derand(x[r] >> 16, rand));
+            if (++k == FRAMES) {
+                k = 0;
+                ++blk;
+            }
+            if (f + 1 < f1) load_frame(in32, blk, k, x);   // prefetch the next frame
+            dft16<-1>(a, v);
+        }
+        __syncthreads();   // the previous frame's last LDS reads are done
+#pragma unroll
+        for (int r = 0; r < 16; r++) lds[16 * t + (r ^ x15)] = v[r];          // swz(16t + r)
+        __syncthreads();
+        // ---- forward pass 1 (R16, NS16): table twiddles W_256^{(t%16) r} ----
+        {
+            float2 a[16];
+#pragma unroll
+            for (int r = 0; r < 16; r++) a[r] = lds[sT + NT * r];
+#pragma unroll
+            for (int r = 1; r < 16; r++) a[r] = cmul(a[r], tp1[(r - 1) * 16 + x15]);
+            dft16<-1>(a, v);
+        }
+        __syncthreads();
+        {
+            const int b1 = (t >> 4) * 256;                                     // swz(b1 + x15 + 16 r)
+#pragma unroll
+            for (int r = 0; r < 16; r++) lds[b1 + 16 * r + (x15 ^ r)] = v[r];
+        }
+        __syncthreads();
+        // ---- forward pass 2 (R16, NS256): recurrence twiddles W_4096^{t r} ----
+        {
+            float2 a[16];
+#pragma unroll
+            for (int r = 0; r < 16; r++) a[r] = lds[sT + NT * r];
+            twiddle_rec16<-1>(a, fw1, fw4);
+            dft16<-1>(a, v);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < 16; r++) lds[sT + NT * r] = v[r];   // Z, natural order
+        __syncthreads();
+
+        if constexpr (N >= 512) {
+            constexpr int R0 = N / 256;
+            // ---- inverse pass 0 (R0, NS1): r2c split x filter, bins tb-N/2 .. tb+N/2 ----
+            float2 u[16];
+            {
+                const int b0 = tunebin + t;                  // bin of r = 0
+                const int sb0 = swz(b0);                     // swz(b0 + 256 r - N w) = sb0 + 256 r - N w
+                const int sc0 = swz(HALF - b0);              // mirror bin, same separability
+                float2 a[R0];
+#pragma unroll
+                for (int r = 0; r < R0; r++) {
+                    const bool wrap = (NT * r >= N / 2);
+                    const int sh = NT * r - (wrap ? N : 0);
+                    const int bin = b0 + sh;
+                    const int q = (r - (wrap ? N / NT : 0)) & 31;       // W_8192^{256 r - N wrap}
+                    // branch-free: read a clamped (valid) address, zero the result if out of range
+                    const bool ok = (unsigned)bin < (unsigned)HALF;
+                    const float2 zk = lds[(sb0 + sh) & (HALF - 1)];
+                    const float2 zc = lds[(sc0 - sh) & (HALF - 1)];
+                    const float2 A = make_float2(zk.x + zc.x, zk.y - zc.y);
+                    const float2 Bi = make_float2(zk.y + zc.y, zc.x - zk.x);   // (Zk - conj Zc)/i
+                    const float2 wb = cmul(pb, make_float2(kW32re[q], kW32im[q]));
+                    const float2 val = cmul(cadd(A, cmul(Bi, wb)), hs[t + NT * r]);
+                    a[r] = ok ? val : make_float2(0.f, 0.f);
+                }
+                dft<R0, +1>(a, u);
+            }
+            __syncthreads();
+            if constexpr (R0 == 16) {
+#pragma unroll
+                for (int r = 0; r < 16; r++) lds[16 * t + (r ^ x15)] = u[r];
+            } else {
+#pragma unroll
+                for (int r = 0; r < R0; r++) lds[swz(R0 * t + r)] = u[r];
+            }
+            __syncthreads();
+            // ---- inverse pass 1 (R16, NS = R0): table twiddles W_{16 R0}^{(j%R0) r} ----
+            constexpr int NB = N / 16;
+            const bool act = (NB == NT) || t < NB;
+            if (act) {
+                float2 a[16];
+                if constexpr (NB == NT) {
+#pragma unroll
+                    for (int r = 0; r < 16; r++) a[r] = lds[sT + NT * r];
+                } else {
+#pragma unroll
+                    for (int r = 0; r < 16; r++) a[r] = lds[swz(t + NB * r)];
+                }
+#pragma unroll
+                for (int r = 1; r < 16; r++) a[r] = cmulc(a[r], tq1[(r - 1) * R0 + (t % R0)]);
+                dft16<+1>(a, u);
+            }
+            __syncthreads();
+            if (act) {
+                if constexpr (R0 == 16) {
+                    const int b1 = (t >> 4) * 256;
+#pragma unroll
+                    for (int r = 0; r < 16; r++) lds[b1 + 16 * r + (x15 ^ r)] = u[r];
+                } else {
+                    const int base = (t / R0) * (16 * R0) + (t % R0);
+#pragma unroll
+                    for (int r = 0; r < 16; r++) lds[swz(base + R0 * r)] = u[r];
+                }
+            }
+            __syncthreads();
+            // ---- inverse pass 2 (R16, NS = N/16): recurrence twiddles, overlap-discard write ----
+            if (act) {
+                float2 a[16];
+                if constexpr (NB == NT) {
+#pragma unroll
+                    for (int r = 0; r < 16; r++) a[r] = lds[sT + NT * r];
+                } else {
+#pragma unroll
+                    for (int r = 0; r < 16; r++) a[r] = lds[swz(t + NB * r)];
+                }
+                twiddle_rec16<+1>(a, iw1, iw4);
+                dft16<+1>(a, u);
+                if (kc == 0) {
+#pragma unroll
+                    for (int r = 4; r < 12; r++) emit<N>(out_blk, 0, t + NB * r, u[r], cs);
+                } else {
+#pragma unroll
+                    for (int r = 0; r < 12; r++) emit<N>(out_blk, kc, t + NB * r, u[r], cs);
+                }
+            }
+        } else {
+            // ---- N <= 256: materialise the N filtered bins, then [N/16, 16] ----
+            constexpr int R0 = N / 16;
+            float2 tv = make_float2(0.f, 0.f);
+            if (t < N) {
+                const int m = t;
+                const int bin = tunebin + m - (m >= N / 2 ? N : 0);
+                tv = split_bin(lds, bin, pst[bin & 8191], hs[m]);
+            }
+            __syncthreads();
+            if (t < N) lds[swz(t)] = tv;
+            __syncthreads();
+            float2 u[16];
+            if (t < 16) {
+                float2 a[R0];
+#pragma unroll
+                for (int r = 0; r < R0; r++) a[r] = lds[swz(t + 16 * r)];
+                dft<R0, +1>(a, u);
+            }
+            __syncthreads();
+            if (t < 16) {
+#pragma unroll
+                for (int r = 0; r < R0; r++) lds[swz(R0 * t + r)] = u[r];
+            }
+            __syncthreads();
+            constexpr int NB = N / 16;   // = R0
+            if (t < NB) {
+                float2 a[16];
+#pragma unroll
+                for (int r = 0; r < 16; r++) a[r] = lds[swz(t + NB * r)];
+#pragma unroll
+                for (int r = 1; r < 16; r++) a[r] = cmulc(a[r], tq1[(r - 1) * NB + t]);
+                dft16<+1>(a, u);
+                if (kc == 0) {
+#pragma unroll
+                    for (int r = 4; r < 12; r++) emit<N>(out_blk, 0, t + NB * r, u[r], cs);
+                } else {
+#pragma unroll
+                    for (int r = 0; r < 12; r++) emit<N>(out_blk, kc, t + NB * r, u[r], cs);
+                }
+            }
+        }
+    }
+}
+
+int g_occupancy[7] = {0, 0, 0, 0, 0, 0, 0};
+int g_cus = 0;
+
+template <int D>
+hipError_t launch_d(const KernelTables &t, const int16_t *d_in, int nblk, float *d_out, int tunebin,
+                    int lsb, int rand, int device, hipStream_t s)
+{
+    if (g_occupancy[D] == 0) {
+        int nb = 0;
+        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, r2iq_persistent_kernel<D>, NT, 0);
+        if (e != hipSuccess) return e;
+        int cus = 0;
+        e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+        if (e != hipSuccess) return e;
+        g_cus = cus;
+        g_occupancy[D] = nb > 0 ? nb : 1;
+    }
+    const int nframes = nblk * FRAMES;
+    int grid = g_cus * g_occupancy[D];
+    if (grid > nframes) grid = nframes;
+    hipLaunchKernelGGL(r2iq_persistent_kernel<D>, dim3((unsigned)grid), dim3(NT), 0, s,
+                       reinterpret_cast<const int *>(d_in), reinterpret_cast<float2 *>(d_out), nframes,
+                       t.tw_p1, t.tw_q1[D], t.rec_f, t.rec_i[D], t.post8192, t.hsel[D], tunebin, lsb, rand);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_frames_persistent(const KernelTables &t, int d, const int16_t *d_in, int nblk, float *d_out,
+                                    int tunebin, int lsb, int rand, int device, hipStream_t s)
+{
+    switch (d) {
+    case 0: return launch_d<0>(t, d_in, nblk, d_out, tunebin, lsb, rand, device, s);
+    case 1: return launch_d<1>(t, d_in, nblk, d_out, tunebin, lsb, rand, device, s);
+    case 2: return launch_d<2>(t, d_in, nblk, d_out, tunebin, lsb, rand, device, s);
+    case 3: return launch_d<3>(t, d_in, nblk, d_out, tunebin, lsb, rand, device, s);
+    case 4: return launch_d<4>(t, d_in, nblk, d_out, tunebin, lsb, rand, device, s);
+    case 5: return launch_d<5>(t, d_in, nblk, d_out, tunebin, lsb, rand, device, s);
+    case 6: return launch_d<6>(t, d_in, nblk, d_out, tunebin, lsb, rand, device, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace sddc

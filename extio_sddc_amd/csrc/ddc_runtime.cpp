@@ -20,6 +20,7 @@
 #include "ddc_kernels.h"
 #include "filterbank.h"
 #include "sddc_ddc.h"
+#include "sddc_ddc_internal.h"
 
 namespace {
 
@@ -71,6 +72,7 @@ struct sddc_ddc {
     int device = 0;
     float gain = 0.f;
     int d = 0, lsb = 0, rand = 0, tunebin = SDDC_DDC_HALF_FFT / 4;   // ctor: mtunebin = halfFft/4
+    int variant = 0;                       // 0: persistent (v2), 1: one workgroup per frame (v1)
     sddc::KernelTables tables;
     float2 *d_tables = nullptr;
 
@@ -150,32 +152,48 @@ int sddc_ddc_create(float gain, int device, sddc_ddc_t **out)
     h->device = device;
     h->gain = gain;
 
-    // tables: tw4096 | post8192 | hsel[0..6]
-    size_t nsel = 0;
-    for (int d = 0; d < SDDC_DDC_NDEC; d++) nsel += (size_t)(SDDC_DDC_HALF_FFT >> d);
-    const size_t ntab = 2 * (size_t)SDDC_DDC_HALF_FFT + nsel;
-    std::vector<float2> host(ntab);
-    for (int k = 0; k < SDDC_DDC_HALF_FFT; k++) {
-        const double a = -2.0 * M_PI * (double)k / 4096.0;
-        const double b = -2.0 * M_PI * (double)k / 8192.0;
-        host[k] = make_float2((float)std::cos(a), (float)std::sin(a));
-        host[SDDC_DDC_HALF_FFT + k] = make_float2((float)std::cos(b), (float)std::sin(b));
+    // ---- constant tables (one device allocation) ----
+    auto W = [](double num, double den) {   // e^{-2 pi i num/den}, double -> float once
+        const double a = -2.0 * M_PI * num / den;
+        return make_float2((float)std::cos(a), (float)std::sin(a));
+    };
+    std::vector<float2> host;
+    auto put = [&](size_t n) { size_t o = host.size(); host.resize(o + n, make_float2(0.f, 0.f)); return o; };
+    const size_t o_tw4096 = put(4096), o_post = put(8192), o_p1 = put(15 * 16), o_recf = put(2 * 256);
+    for (int k = 0; k < 4096; k++) host[o_tw4096 + k] = W(k, 4096);
+    for (int k = 0; k < 8192; k++) host[o_post + k] = W(k, 8192);
+    for (int r = 1; r < 16; r++)
+        for (int s = 0; s < 16; s++) host[o_p1 + (r - 1) * 16 + s] = W((double)s * r, 256);
+    for (int j = 0; j < 256; j++) {
+        host[o_recf + j] = W(j, 4096);
+        host[o_recf + 256 + j] = W(4.0 * j, 4096);
     }
-    size_t off = 2 * (size_t)SDDC_DDC_HALF_FFT;
-    size_t sel_off[SDDC_DDC_NDEC];
+    size_t o_hsel[SDDC_DDC_NDEC], o_q1[SDDC_DDC_NDEC], o_reci[SDDC_DDC_NDEC];
     std::vector<std::complex<double>> H(SDDC_DDC_HALF_FFT);
     for (int d = 0; d < SDDC_DDC_NDEC; d++) {
-        sddc::filter_response(gain, d, H.data());
         const int mfft = SDDC_DDC_HALF_FFT >> d;
-        sel_off[d] = off;
+        sddc::filter_response(gain, d, H.data());
+        o_hsel[d] = put(mfft);
         for (int m = 0; m < mfft; m++) {
             // inverse-input position m: H[m] (m < mfft/2), H[4096 - mfft + m] otherwise
             // (impl.hpp:90,94 with filter2 = filter + halfFft - mfft/2, impl.hpp:7)
             const std::complex<double> v = H[m < mfft / 2 ? m : SDDC_DDC_HALF_FFT - mfft + m];
-            host[off + m] = make_float2((float)(0.5 * v.real()), (float)(0.5 * v.imag()));
+            host[o_hsel[d] + m] = make_float2((float)(0.5 * v.real()), (float)(0.5 * v.imag()));
         }
-        off += (size_t)mfft;
+        // inverse pass-1 table W_{16S}^{s r}, S = mfft/256 (mfft >= 512) or mfft/16
+        const int S = mfft >= 512 ? mfft / 256 : mfft / 16;
+        o_q1[d] = put(15 * (size_t)S);
+        for (int r = 1; r < 16; r++)
+            for (int s = 0; s < S; s++) host[o_q1[d] + (r - 1) * S + s] = W((double)s * r, 16.0 * S);
+        // inverse pass-2 recurrence bases W_N^j, W_N^{4j}, j < N/16 (mfft >= 512)
+        o_reci[d] = put(2 * 256);
+        if (mfft >= 512)
+            for (int j = 0; j < mfft / 16; j++) {
+                host[o_reci[d] + j] = W(j, mfft);
+                host[o_reci[d] + 256 + j] = W(4.0 * j, mfft);
+            }
     }
+    const size_t ntab = host.size();
     hipError_t e = hipMalloc(&h->d_tables, ntab * sizeof(float2));
     if (e == hipSuccess) e = hipMemcpy(h->d_tables, host.data(), ntab * sizeof(float2), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
@@ -183,9 +201,16 @@ int sddc_ddc_create(float gain, int device, sddc_ddc_t **out)
         sddc_ddc_destroy(h);
         return fail(SDDC_ERR_HIP, "create: %s", hipGetErrorString(e));
     }
-    h->tables.tw4096 = h->d_tables;
-    h->tables.post8192 = h->d_tables + SDDC_DDC_HALF_FFT;
-    for (int d = 0; d < SDDC_DDC_NDEC; d++) h->tables.hsel[d] = h->d_tables + sel_off[d];
+    const float2 *T = h->d_tables;
+    h->tables.tw4096 = T + o_tw4096;
+    h->tables.post8192 = T + o_post;
+    h->tables.tw_p1 = T + o_p1;
+    h->tables.rec_f = T + o_recf;
+    for (int d = 0; d < SDDC_DDC_NDEC; d++) {
+        h->tables.hsel[d] = T + o_hsel[d];
+        h->tables.tw_q1[d] = T + o_q1[d];
+        h->tables.rec_i[d] = T + o_reci[d];
+    }
     *out = h;
     return SDDC_OK;
 }
@@ -264,6 +289,22 @@ int sddc_ddc_reset(sddc_ddc_t *h)
     return SDDC_OK;
 }
 
+static hipError_t launch_single(sddc_ddc_t *h, const int16_t *d_in, int nblk, float *d_out, hipStream_t s)
+{
+    if (h->variant == 1)
+        return sddc::launch_frames(h->tables, h->d, d_in, nblk, d_out, h->tunebin, h->lsb, h->rand, s);
+    return sddc::launch_frames_persistent(h->tables, h->d, d_in, nblk, d_out, h->tunebin, h->lsb, h->rand,
+                                          h->device, s);
+}
+
+/* internal (not in include/sddc_ddc.h): kernel variant for A/B timing, see sddc_ddc_internal.h */
+int sddc_ddc_internal_set_variant(sddc_ddc_t *h, int variant)
+{
+    if (!h || variant < 0 || variant > 1) return fail(SDDC_ERR_ARG, "bad variant");
+    h->variant = variant;
+    return SDDC_OK;
+}
+
 static int check_process_args(sddc_ddc_t *h, const int16_t *in, int nblk, const void *out)
 {
     if (!h) return fail(SDDC_ERR_ARG, "null handle");
@@ -280,8 +321,7 @@ int sddc_ddc_process_device(sddc_ddc_t *h, const int16_t *d_in, int nblk, float 
     if (rc) return rc;
     DeviceGuard g(h->device);
     HIP_TRY(g.err);
-    HIP_TRY(sddc::launch_frames(h->tables, h->d, d_in, nblk, d_out, h->tunebin, h->lsb, h->rand,
-                                (hipStream_t)hip_stream));
+    HIP_TRY(launch_single(h, d_in, nblk, d_out, (hipStream_t)hip_stream));
     return SDDC_OK;
 }
 
@@ -336,8 +376,7 @@ int sddc_ddc_process_host(sddc_ddc_t *h, const int16_t *in, int nblk, float *out
         const size_t nin = kHistory + (size_t)n * kBlock;
         std::memcpy(h->h_in + kHistory, in + (size_t)done * kBlock, (size_t)n * kBlock * sizeof(int16_t));
         HIP_TRY(hipMemcpyAsync(h->d_in, h->h_in, nin * sizeof(int16_t), hipMemcpyHostToDevice, h->stream));
-        HIP_TRY(sddc::launch_frames(h->tables, h->d, h->d_in, n, h->d_out, h->tunebin, h->lsb, h->rand,
-                                    h->stream));
+        HIP_TRY(launch_single(h, h->d_in, n, h->d_out, h->stream));
         HIP_TRY(hipMemcpyAsync(h->h_out, h->d_out, (size_t)n * per_blk_out * sizeof(float),
                                hipMemcpyDeviceToHost, h->stream));
         HIP_TRY(hipStreamSynchronize(h->stream));

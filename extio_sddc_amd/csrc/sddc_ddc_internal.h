@@ -1,0 +1,12 @@
+// sddc_ddc_internal.h — development-only entry points (not part of the C ABI contract).
+#pragma once
+#include "sddc_ddc.h"
+#ifdef __cplusplus
+extern "C" {
+#endif
+/* Select the single-channel kernel: 0 = persistent (default), 1 = one workgroup per
+ * frame.  Used by tools/ab_kernels.py to time variants in one process. */
+int sddc_ddc_internal_set_variant(sddc_ddc_t *h, int variant);
+#ifdef __cplusplus
+}
+#endif
