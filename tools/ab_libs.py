@@ -1,0 +1,81 @@
+#!/usr/bin/env python3
+"""A/B timing of several builds of libsddc_ddc.so in ONE process, interleaved rounds
+(cdna_hip_programming.md §5.4 rule 24).  Each library gets its own handle; all share
+torch's HIP runtime.  Output difference vs the first library is reported too.
+
+  python tools/ab_libs.py --libs build/ab/a.so build/ab/b.so [--d 0 4] [--nblk 2048]
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--libs", nargs="+", required=True)
+    ap.add_argument("--d", type=int, nargs="+", default=[0, 1, 2, 3, 4])
+    ap.add_argument("--nblk", type=int, default=2048)
+    ap.add_argument("--rounds", type=int, default=10)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--tunebin", type=int, default=1024)
+    args = ap.parse_args()
+
+    import torch
+    from extio_sddc_amd._lib import SIGNATURES
+    dev = torch.device("cuda", 0)
+    libs, handles = [], []
+    for p in args.libs:
+        L = ctypes.CDLL(os.path.abspath(p))
+        for name, (res, a) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype, fn.argtypes = res, a
+        h = ctypes.c_void_p()
+        rc = L.sddc_ddc_create(1.0, 0, ctypes.byref(h))
+        assert rc == 0, L.sddc_ddc_last_error()
+        L.sddc_ddc_set_tunebin(h, args.tunebin)
+        libs.append(L)
+        handles.append(h)
+    nblk = args.nblk
+    g = torch.Generator(device=dev).manual_seed(0x5DDC)
+    d_in = torch.randint(-32768, 32767, (4096 + nblk * 65536,), dtype=torch.int16, device=dev, generator=g)
+    s = torch.cuda.current_stream().cuda_stream
+    res = {}
+    for d in args.d:
+        n_out = nblk * (32768 >> d) * 2
+        outs = [torch.empty(n_out, dtype=torch.float32, device=dev) for _ in libs]
+        times = [[] for _ in libs]
+        for L, h in zip(libs, handles):
+            L.sddc_ddc_set_decimation(h, d)
+        for rnd in range(args.rounds + 1):
+            for i, (L, h) in enumerate(zip(libs, handles)):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(args.reps):
+                    rc = L.sddc_ddc_process_device(h, d_in.data_ptr(), nblk, outs[i].data_ptr(), s)
+                    assert rc == 0, L.sddc_ddc_last_error()
+                e1.record()
+                torch.cuda.synchronize()
+                if rnd:
+                    times[i].append(e0.elapsed_time(e1) / args.reps)
+        for i, p in enumerate(args.libs):
+            ts = sorted(times[i])
+            med = ts[len(ts) // 2]
+            diff = ((outs[i] - outs[0]).abs().max() / outs[0].abs().max()).item()
+            gs = nblk * 65536 / (med * 1e-3) / 1e9
+            frac = nblk * 65536 * (2 + 4 / (1 << d)) / (med * 1e-3) / 8e12
+            res[f"d{d}:{os.path.basename(p)}"] = {"median_ms": med, "min_ms": ts[0], "GSps": gs, "hbm_frac": frac,
+                                                  "maxrel_vs_first": diff}
+            print(f"d={d} {os.path.basename(p):28s} median {med:.3f} ms min {ts[0]:.3f}  {gs:7.1f} GS/s  "
+                  f"roofline {frac*100:5.1f}%  maxrel vs first {diff:.2e}", flush=True)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,15 @@
+#!/bin/bash
+# Build a variant of libsddc_ddc.so with extra flags for the persistent kernel into build/ab/NAME.so
+# usage: tools/build_variant.sh NAME "extra hipcc flags" [-DMACRO=...]
+set -e
+R=$(cd "$(dirname "$0")/.." && pwd)
+NAME=$1; EXTRA=$2
+O=$R/build/ab/$NAME; mkdir -p $O
+C=$R/extio_sddc_amd/csrc
+F="-O3 -std=c++17 -fPIC -fno-slp-vectorize -I$C -I$R/include"
+hipcc --offload-arch=gfx950 $F -c $C/ddc_kernels.hip -o $O/k.o
+hipcc --offload-arch=gfx950 $F $EXTRA -c $C/ddc_persistent.hip -o $O/p.o
+hipcc $F -ffp-contract=off -c $C/ddc_runtime.cpp -o $O/r.o
+hipcc $F -ffp-contract=off -c $C/filterbank.cpp -o $O/f.o
+hipcc --offload-arch=gfx950 -shared $O/k.o $O/p.o $O/r.o $O/f.o -o $R/build/ab/$NAME.so
+echo built $R/build/ab/$NAME.so
