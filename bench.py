@@ -145,7 +145,7 @@ def main() -> None:
         samples_per_step_all = nblk * BLOCK * world
         workload = f"single d={d} nblk={nblk}"
     else:
-        from extio_sddc_amd.shard import channel_shard
+        from extio_sddc_amd.shard import broadcast_samples, channel_shard
         tbs_all = [4 * c for c in range(args.channels)]
         lo, hi = channel_shard(args.channels, world, rank)
         tbs = tbs_all[lo:hi]
@@ -157,7 +157,7 @@ def main() -> None:
 
         def step():
             if world > 1:
-                dist.broadcast(d_in, src=0)
+                broadcast_samples(d_in, src=0)
             ddc.process_channels_device(d_in, nblk, tbs, d_out, stream)
         samples_per_step_all = nblk * BLOCK          # one shared stream
         workload = f"channels d={d} nblk={nblk} nch={args.channels}"

@@ -28,3 +28,12 @@ def segment_samples(lo: int, hi: int) -> tuple[int, int]:
 def channel_shard(nch: int, world: int, rank: int) -> tuple[int, int]:
     """Channels [lo, hi) computed by `rank`."""
     return block_shard(nch, world, rank)
+
+
+def broadcast_samples(buf, src: int = 0) -> None:
+    """Broadcast an int16 sample batch from `src` to every rank.  NCCL/RCCL and gloo have
+    no int16 type, so the (even-length) batch travels as its int32 view — same bytes."""
+    import torch
+    import torch.distributed as dist
+    assert buf.dtype == torch.int16 and buf.numel() % 2 == 0 and buf.is_contiguous()
+    dist.broadcast(buf.view(torch.int32), src=src)

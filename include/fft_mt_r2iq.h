@@ -1,0 +1,75 @@
+/*
+ * fft_mt_r2iq.h — drop-in replacement for ExtIO_sddc's Core/fft_mt_r2iq.h.
+ *
+ * Same class name, base class, constructor and virtual interface as the reference
+ * (Core/fft_mt_r2iq.h:21-31), so RadioHandler (`new fft_mt_r2iq()`,
+ * Core/RadioHandler.cpp:94-95), libsddc, the ExtIO DLL and SoapySDDC build and run
+ * against it unchanged.  The DSP runs on an MI355X through the C ABI in sddc_ddc.h;
+ * FFTW/MKL/Accelerate and the AVX/AVX2/AVX-512/NEON worker variants are gone.
+ *
+ * Behaviour kept from the reference:
+ *   - Init(gain, in, out) designs the 7 filter banks (fft_mt_r2iq.cpp:147-227);
+ *   - TurnOn() latches decimation and sideband, starts both rings and one worker
+ *     (fft_mt_r2iq.cpp:111-129, impl.hpp:3-7); the history starts at zero;
+ *   - updateRand() and setFreqOffset() take effect at the next input block
+ *     (impl.hpp:20,40);
+ *   - each input block yields 32768>>d complex floats; one output ring block
+ *     (EXT_BLOCKLEN = 32768 complex) is released every 2^d input blocks
+ *     (impl.hpp:100-148);
+ *   - TurnOff() stops both rings and joins the worker (fft_mt_r2iq.cpp:131-143).
+ * Different by design: the worker may hand several already-queued input blocks to
+ * the GPU in one launch (never waiting for more than the first); a GPU failure is
+ * reported on stderr and through lastError() and the worker stops (no CPU fallback).
+ */
+#pragma once
+
+#include <atomic>
+#include <cstdint>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "r2iq.h"
+
+/* Core/fft_mt_r2iq.h:18-19 (values of config.h:49,80 — FFTN_R_ADC 8192, transferSize 131072) */
+static const int halfFft = 4096;
+static const int fftPerBuf = 11;
+
+struct sddc_ddc;
+
+class fft_mt_r2iq : public r2iqControlClass {
+public:
+    fft_mt_r2iq();
+    virtual ~fft_mt_r2iq();
+
+    float setFreqOffset(float offset);
+
+    void Init(float gain, ringbuffer<int16_t> *buffers, ringbuffer<float> *obuffers);
+    void TurnOn();
+    void TurnOff(void);
+    bool IsOn(void);
+
+    /* additions (not part of r2iqControlClass) */
+    const char *lastError() const { return last_error_.c_str(); }
+    uint64_t blocksProcessed() const { return blocks_done_.load(); }
+
+private:
+    void worker();
+    void fail(const char *what);
+
+    ringbuffer<int16_t> *inputbuffer = nullptr;
+    ringbuffer<float> *outputbuffer = nullptr;
+    float GainScale = 0.0f;
+    int mfftdim[NDECIDX];
+    std::atomic<int> mtunebin;
+
+    sddc_ddc *ddc_ = nullptr;         /* GPU handle (C ABI) */
+    int device_ = 0;
+    std::thread worker_;
+    std::vector<int16_t> in_stage_;   /* batched input blocks */
+    std::vector<float> out_stage_;    /* their IQ */
+    std::atomic<uint64_t> blocks_done_{0};
+    int wc_base_ = 0;                 /* input ring write count at TurnOn */
+    uint64_t consumed_ = 0;           /* input blocks taken since TurnOn */
+    std::string last_error_;
+};

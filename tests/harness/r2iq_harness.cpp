@@ -1,0 +1,77 @@
+// r2iq_harness.cpp — drives the drop-in fft_mt_r2iq through its r2iqControlClass interface
+// exactly as RadioHandler does (Init -> setDecimate/setSideband/updateRand/setFreqOffset ->
+// TurnOn -> ring traffic -> TurnOff), with the standalone ring (include/sddc_compat).
+// A producer thread writes int16 blocks read from a file into the input ring; the main
+// thread collects the 32768-sample output blocks into a file.  Also probes the base-class
+// byte layout of the private fields (randADC @44, sideband @45, Core/r2iq.h).
+//
+//   r2iq_harness IN.bin NBLK D TUNEBIN LSB RAND GAIN OUT.bin
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "fft_mt_r2iq.h"
+
+int main(int argc, char **argv)
+{
+    if (argc != 9) {
+        std::fprintf(stderr, "usage: %s IN.bin NBLK D TUNEBIN LSB RAND GAIN OUT.bin\n", argv[0]);
+        return 2;
+    }
+    const int nblk = std::atoi(argv[2]), d = std::atoi(argv[3]), tb = std::atoi(argv[4]);
+    const bool lsb = std::atoi(argv[5]) != 0, rnd = std::atoi(argv[6]) != 0;
+    const float gain = (float)std::atof(argv[7]);
+    std::vector<int16_t> data((size_t)nblk * 65536);
+    FILE *in = std::fopen(argv[1], "rb");
+    if (!in || fread(data.data(), sizeof(int16_t), data.size(), in) != data.size()) return 2;
+    std::fclose(in);
+
+    ringbuffer<int16_t> inbuf;           // 64 slots, like RadioHandlerClass::inputbuffer
+    ringbuffer<float> outbuf;
+    inbuf.setBlockSize(65536);
+    outbuf.setBlockSize(32768 * 2 * sizeof(float));   // RadioHandler.cpp:166 (EXT_BLOCKLEN*2*sizeof(float))
+
+    fft_mt_r2iq r;
+    r2iqControlClass *base = &r;
+    base->Init(gain, &inbuf, &outbuf);
+    base->setDecimate(d);
+    base->setSideband(lsb);
+    base->updateRand(rnd);
+    const unsigned char *raw = reinterpret_cast<const unsigned char *>(base);
+    if (raw[44] != (unsigned char)rnd || raw[45] != (unsigned char)lsb) {
+        std::fprintf(stderr, "ABI: randADC/sideband not at bytes 44/45\n");
+        return 5;
+    }
+    const float fc = base->setFreqOffset((float)tb / 4096.0f);
+    base->TurnOn();
+    if (!base->IsOn()) {
+        std::fprintf(stderr, "TurnOn failed: %s\n", r.lastError());
+        return 3;
+    }
+    std::thread producer([&] {
+        for (int b = 0; b < nblk; b++) {
+            int16_t *p = inbuf.getWritePtr();
+            if (!base->IsOn()) return;
+            std::memcpy(p, data.data() + (size_t)b * 65536, 65536 * sizeof(int16_t));
+            inbuf.WriteDone();
+        }
+    });
+    FILE *out = std::fopen(argv[8], "wb");
+    const int want = nblk >> d;
+    int got = 0;
+    for (; got < want; got++) {
+        const float *p = outbuf.getReadPtr();
+        if (!base->IsOn()) break;
+        fwrite(p, sizeof(float), 65536, out);
+        outbuf.ReadDone();
+    }
+    std::fclose(out);
+    base->TurnOff();
+    producer.join();
+    std::printf("output blocks %d of %d, residual fc %g, gpu blocks %llu\n", got, want, fc,
+                (unsigned long long)r.blocksProcessed());
+    return got == want ? 0 : 4;
+}

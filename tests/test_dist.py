@@ -1,0 +1,101 @@
+"""N>1 data paths on CPU with gloo, world_size 2.
+
+- time segments (weak/strong scaling of one stream): each rank processes its own block
+  range plus the 4096-sample halo; gathered outputs concatenate to the whole-stream result
+  bit-exactly (blocks only depend on their own samples and the history).
+- channels (C5): rank 0 owns the int16 batch and broadcasts it (the xGMI/RCCL step on the
+  GPU node; gloo here); each rank computes its contiguous channel shard; the gathered
+  shards equal every channel computed on one rank.
+The per-rank compute here is the oracle (no GPU); the partitioning, halo and collective
+logic is extio_sddc_amd.shard, the same code bench.py uses on the GPUs.
+"""
+from __future__ import annotations
+
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, mode, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from extio_sddc_amd.shard import block_shard, broadcast_samples, channel_shard, segment_samples
+        from extio_sddc_amd.synth import make_stream
+        from oracle import oracle as O
+        if mode == "segments":
+            nblk, d, tb = 5, 1, 1024
+            x = make_stream(nblk, "mix")
+            lo, hi = block_shard(nblk, world, rank)
+            s0, s1 = segment_samples(lo, hi)
+            y = O.r2iq(x[s0:s1], hi - lo, d, tb) if hi > lo else np.zeros(0, np.complex128)
+            parts = [None] * world
+            dist.all_gather_object(parts, (lo, hi, y))
+            if rank == 0:
+                full = O.r2iq(x, nblk, d, tb)
+                cat = np.concatenate([p[2] for p in sorted(parts, key=lambda p: p[0])])
+                q.put(bool(np.array_equal(cat, full)) and sum(p[1] - p[0] for p in parts) == nblk)
+        else:
+            nblk, d, nch = 2, 4, 6
+            tbs = [4 * (97 * c % 1024) for c in range(nch)]
+            buf = torch.zeros(4096 + nblk * 65536, dtype=torch.int16)
+            if rank == 0:
+                buf.copy_(torch.from_numpy(make_stream(nblk, "uniform")))
+            broadcast_samples(buf, src=0)
+            x = buf.numpy()
+            lo, hi = channel_shard(nch, world, rank)
+            H = O.filter_bank(1.0)
+            mine = [O.r2iq(x, nblk, d, tbs[c], H=H) for c in range(lo, hi)]
+            parts = [None] * world
+            dist.all_gather_object(parts, (lo, mine))
+            if rank == 0:
+                got = [y for p in sorted(parts, key=lambda p: p[0]) for y in p[1]]
+                ok = len(got) == nch and all(np.array_equal(got[c], O.r2iq(x, nblk, d, tbs[c], H=H))
+                                             for c in range(nch))
+                q.put(ok)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["segments", "channels"])
+def test_two_rank_gloo(mode):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, mode, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+        assert p.exitcode == 0
+    assert q.get(timeout=10) is True
+
+
+def test_shard_partitions():
+    from extio_sddc_amd.shard import block_shard, channel_shard, segment_samples
+    for n in (1, 7, 2048):
+        for w in (1, 2, 3, 8):
+            spans = [block_shard(n, w, r) for r in range(w)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(spans[i][1] == spans[i + 1][0] for i in range(w - 1))
+            assert max(b - a for a, b in spans) - min(b - a for a, b in spans) <= 1
+    assert channel_shard(1024, 8, 3) == (384, 512)
+    assert segment_samples(2, 5) == (2 * 65536, 4096 + 5 * 65536)

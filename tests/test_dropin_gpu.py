@@ -1,0 +1,67 @@
+"""The drop-in boundary on a real MI355X: fft_mt_r2iq driven through r2iqControlClass.
+
+1. build/bin/r2iq_harness — the class driven exactly as RadioHandler drives it, over the
+   standalone ring (include/sddc_compat), checked against the f64 oracle.
+2. oracle/_ref/radiohandler_harness — the REFERENCE's unchanged RadioHandlerClass
+   (Core/RadioHandler.cpp, built by `make -C oracle radiohandler` where the reference is
+   mounted) with a mock USB producer, running our class end to end; output taken from the
+   user callback (RadioHandler.cpp:51).  Skipped when that binary was not built.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from extio_sddc_amd.synth import make_stream
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HARNESS = os.path.join(ROOT, "build", "bin", "r2iq_harness")
+RH_HARNESS = os.path.join(ROOT, "oracle", "_ref", "radiohandler_harness")
+TOL = 1e-5
+BBRF103_GAINFACTOR = np.float32(7.8e-8)   # DummyRadio's gain (Core/RadioHandler.h:143, config.h:57)
+
+
+def _run(cmd, timeout=120):
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout)
+    assert p.returncode == 0, f"{cmd[0]} rc={p.returncode}\n{p.stdout}\n{p.stderr}"
+    return p.stdout
+
+
+@pytest.mark.parametrize("d,tb,lsb,rand,src,nblk", [
+    (0, 1024, 0, 0, "mix", 6),
+    (1, 1024, 1, 1, "mix", 8),      # C4: decim 4, sideband invert, rand
+    (2, 284, 0, 0, "uniform", 8),
+    (4, 3888, 1, 0, "mix", 32),     # 2^4 input blocks per output block
+])
+def test_dropin_class(tmp_path, oracle, d, tb, lsb, rand, src, nblk):
+    assert os.path.exists(HARNESS), "build/bin/r2iq_harness missing (make -C extio_sddc_amd/csrc)"
+    x = make_stream(nblk, src)
+    fin, fout = tmp_path / "in.bin", tmp_path / "out.bin"
+    x[4096:].tofile(fin)
+    _run([HARNESS, str(fin), str(nblk), str(d), str(tb), str(lsb), str(rand), "1.0", str(fout)])
+    y = np.fromfile(fout, np.float32).view(np.complex64)
+    ref = oracle.r2iq(x, nblk, d, tb, lsb, rand)
+    assert y.size == ref.size == nblk * (32768 >> d)
+    assert oracle.max_rel_err(y, ref) <= TOL
+
+
+@pytest.mark.skipif(not os.path.exists(RH_HARNESS), reason="reference RadioHandler harness not built here")
+@pytest.mark.parametrize("srate_idx,tune_hz,rand", [(4, 8_000_000, 0), (3, 5_000_000, 1), (0, 8_000_000, 0)])
+def test_reference_radiohandler_runs_dropin(tmp_path, oracle, srate_idx, tune_hz, rand):
+    d = 4 - srate_idx                        # RadioHandler.cpp:152 (adc 64 MHz)
+    nblk = max(4, 2 << d)
+    x = make_stream(nblk, "mix")
+    fin, fout = tmp_path / "in.bin", tmp_path / "out.bin"
+    x[4096:].tofile(fin)
+    _run([RH_HARNESS, str(fin), str(nblk), str(srate_idx), str(tune_hz), str(rand), str(fout)])
+    y = np.fromfile(fout, np.float32).view(np.complex64)
+    tb, fc = oracle.set_freq_offset(np.float32(tune_hz / 32e6), d)
+    assert fc == 0.0                         # exact tune: no fine-tune NCO in OnDataPacket
+    ref = oracle.r2iq(x, nblk, d, tb, False, rand, gain=float(BBRF103_GAINFACTOR))
+    assert y.size == ref.size                # every callback carries 32768 samples (core_test.cpp:167)
+    assert oracle.max_rel_err(y, ref) <= TOL
