@@ -51,10 +51,15 @@ __device__ __forceinline__ int swz(int e) { return e ^ ((e >> 4) & 15); }
 template <int DIR>
 __device__ __forceinline__ float2 tmul(float2 a, float2 w) { return DIR < 0 ? cmul(a, w) : cmulc(a, w); }
 
-__device__ __forceinline__ float derand(int v, int rand)
+// convert_float<rand>, Core/fft_mt_r2iq.h:36-51.  With RAND the odd int16 samples are XORed
+// with 0xFFFE, which for an odd 16-bit value is exactly its negation (v ^ 0xFFFE = ~v ^ 1 = -v),
+// so the de-randomised float is (v odd ? -v : v): a sign-bit XOR with the sample's LSB.
+template <bool RAND>
+__device__ __forceinline__ float derand(int v)
 {
-    // convert_float<rand>, Core/fft_mt_r2iq.h:36-51: odd samples XOR 0xFFFE when rand is on
-    return (float)(v ^ (-2 & -(v & rand & 1)));
+    const float f = (float)v;
+    if constexpr (!RAND) return f;
+    return __int_as_float(__float_as_int(f) ^ (v << 31));
 }
 
 // a[r] *= W^{r} for r = 1..15 given the forward-direction W^1 and W^4 of this lane
@@ -97,10 +102,10 @@ __device__ __forceinline__ float2 split_bin(const float2 *lds, int bin, float2 w
     return cmul(cadd(A, cmul(Bi, wbin)), hh);
 }
 
-template <int N>
-__device__ __forceinline__ void emit(float2 *__restrict__ out_blk, int k, int n, float2 v, float cs)
+template <int N, bool LSB>
+__device__ __forceinline__ void emit(float2 *__restrict__ out_blk, int k, int n, float2 v)
 {
-    v.y *= cs;
+    if constexpr (LSB) v.y = -v.y;   // copy<flip=true>, fft_mt_r2iq.h:63-71
     if (k == 0)
         out_blk[n - N / 4] = v;
     else
@@ -114,13 +119,13 @@ __device__ __forceinline__ void load_frame(const int *__restrict__ in32, int blk
     for (int r = 0; r < 16; r++) x[r] = p[NT * r];
 }
 
-template <int D>
+template <int D, bool RAND, bool LSB>
 __global__ __launch_bounds__(NT, 2) void r2iq_persistent_kernel(
     const int *__restrict__ in32, float2 *__restrict__ out, int nframes,
     const float2 *__restrict__ tw_p1, const float2 *__restrict__ tw_q1,
     const float2 *__restrict__ rec_f, const float2 *__restrict__ rec_i,
     const float2 *__restrict__ post8192, const float2 *__restrict__ hsel,
-    int tunebin, int lsb, int rand)
+    int tunebin)
 {
     constexpr int N = HALF >> D;
     __shared__ __attribute__((aligned(16))) float2 lds[HALF];
@@ -141,7 +146,6 @@ __global__ __launch_bounds__(NT, 2) void r2iq_persistent_kernel(
         }
     }
     const float2 pb_ = post8192[(tunebin + tid) & 8191];   // W_8192^{tb + tid}
-    const float cs = lsb ? -1.f : 1.f;
 
     int blk = f0 / FRAMES, k = f0 - blk * FRAMES;
     int x[16];
@@ -167,7 +171,7 @@ __global__ __launch_bounds__(NT, 2) void r2iq_persistent_kernel(
             float2 a[16];
 #pragma unroll
             for (int r = 0; r < 16; r++)
-                a[r] = make_float2(derand((int)(short)(x[r] & 0xffff), rand), derand(x[r] >> 16, rand));
+                a[r] = make_float2(derand<RAND>((int)(short)(x[r] & 0xffff)), derand<RAND>(x[r] >> 16));
             if (++k == FRAMES) {
                 k = 0;
                 ++blk;
@@ -287,10 +291,10 @@ __global__ __launch_bounds__(NT, 2) void r2iq_persistent_kernel(
                 dft16<+1>(a, u);
                 if (kc == 0) {
 #pragma unroll
-                    for (int r = 4; r < 12; r++) emit<N>(out_blk, 0, t + NB * r, u[r], cs);
+                    for (int r = 4; r < 12; r++) emit<N, LSB>(out_blk, 0, t + NB * r, u[r]);
                 } else {
 #pragma unroll
-                    for (int r = 0; r < 12; r++) emit<N>(out_blk, kc, t + NB * r, u[r], cs);
+                    for (int r = 0; r < 12; r++) emit<N, LSB>(out_blk, kc, t + NB * r, u[r]);
                 }
             }
         } else {
@@ -328,40 +332,53 @@ __global__ __launch_bounds__(NT, 2) void r2iq_persistent_kernel(
                 dft16<+1>(a, u);
                 if (kc == 0) {
 #pragma unroll
-                    for (int r = 4; r < 12; r++) emit<N>(out_blk, 0, t + NB * r, u[r], cs);
+                    for (int r = 4; r < 12; r++) emit<N, LSB>(out_blk, 0, t + NB * r, u[r]);
                 } else {
 #pragma unroll
-                    for (int r = 0; r < 12; r++) emit<N>(out_blk, kc, t + NB * r, u[r], cs);
+                    for (int r = 0; r < 12; r++) emit<N, LSB>(out_blk, kc, t + NB * r, u[r]);
                 }
             }
         }
     }
 }
 
-int g_occupancy[7] = {0, 0, 0, 0, 0, 0, 0};
+int g_occupancy[7][4] = {};
 int g_cus = 0;
 
-template <int D>
-hipError_t launch_d(const KernelTables &t, const int16_t *d_in, int nblk, float *d_out, int tunebin,
-                    int lsb, int rand, int device, hipStream_t s)
+template <int D, bool RAND, bool LSB>
+hipError_t launch_v(const KernelTables &t, const int16_t *d_in, int nblk, float *d_out, int tunebin,
+                    int device, hipStream_t s)
 {
-    if (g_occupancy[D] == 0) {
+    auto kern = r2iq_persistent_kernel<D, RAND, LSB>;
+    int &occ = g_occupancy[D][(RAND ? 2 : 0) + (LSB ? 1 : 0)];
+    if (occ == 0) {
         int nb = 0;
-        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, r2iq_persistent_kernel<D>, NT, 0);
+        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, NT, 0);
         if (e != hipSuccess) return e;
         int cus = 0;
         e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
         if (e != hipSuccess) return e;
         g_cus = cus;
-        g_occupancy[D] = nb > 0 ? nb : 1;
+        occ = nb > 0 ? nb : 1;
     }
     const int nframes = nblk * FRAMES;
-    int grid = g_cus * g_occupancy[D];
+    int grid = g_cus * occ;
     if (grid > nframes) grid = nframes;
-    hipLaunchKernelGGL(r2iq_persistent_kernel<D>, dim3((unsigned)grid), dim3(NT), 0, s,
-                       reinterpret_cast<const int *>(d_in), reinterpret_cast<float2 *>(d_out), nframes,
-                       t.tw_p1, t.tw_q1[D], t.rec_f, t.rec_i[D], t.post8192, t.hsel[D], tunebin, lsb, rand);
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), 0, s, reinterpret_cast<const int *>(d_in),
+                       reinterpret_cast<float2 *>(d_out), nframes, t.tw_p1, t.tw_q1[D], t.rec_f, t.rec_i[D],
+                       t.post8192, t.hsel[D], tunebin);
     return hipGetLastError();
+}
+
+template <int D>
+hipError_t launch_d(const KernelTables &t, const int16_t *d_in, int nblk, float *d_out, int tunebin,
+                    int lsb, int rand, int device, hipStream_t s)
+{
+    if (rand)
+        return lsb ? launch_v<D, true, true>(t, d_in, nblk, d_out, tunebin, device, s)
+                   : launch_v<D, true, false>(t, d_in, nblk, d_out, tunebin, device, s);
+    return lsb ? launch_v<D, false, true>(t, d_in, nblk, d_out, tunebin, device, s)
+               : launch_v<D, false, false>(t, d_in, nblk, d_out, tunebin, device, s);
 }
 
 }  // namespace
