@@ -20,6 +20,8 @@ struct KernelTables {
     const float2 *tw_q1[7] = {};       // [15][S]:  W_{16S}^{s r}   inverse pass 1, S = NS of that pass
     const float2 *rec_f = nullptr;     // [2][256]: W_4096^{j}, W_4096^{4j}  forward pass 2 recurrence
     const float2 *rec_i[7] = {};       // [2][256]: W_N^{j}, W_N^{4j}        inverse pass 2 (N >= 512)
+    const float2 *twt_f = nullptr;     // [15][256]: W_4096^{j r}   forward pass 2 twiddles (table form)
+    const float2 *twt_i[7] = {};       // [15][N/16]: W_N^{j r}     inverse pass 2 twiddles (N >= 512)
 };
 
 // v1: one workgroup per frame (kept as a reference variant for A/B timing)

@@ -29,6 +29,24 @@ constexpr int HALF = 4096;
 constexpr int HOP = 6144;
 constexpr int BLOCK = 65536;
 constexpr int FRAMES = 11;
+#ifndef SDDC_DB
+#define SDDC_DB 0
+#endif
+// Double-buffered LDS (two 32 KB frames, one barrier per pass) vs one buffer (two
+// barriers per pass, twice the workgroups per CU).  Build-time switch for A/B timing.
+constexpr bool kDB = SDDC_DB != 0;
+#ifndef SDDC_WAVES
+#define SDDC_WAVES 2          // __launch_bounds__ min waves per SIMD
+#endif
+#ifndef SDDC_TWTAB
+#define SDDC_TWTAB 0          // NS=N/16 passes: 1 = coalesced [r][t] twiddle table, 0 = register recurrence
+#endif
+#ifndef SDDC_FAKE
+#define SDDC_FAKE 0           // timing-only builds: 1 = no hsel loads, 2 = no tp1/tq1 loads, 3 = neither
+#endif
+#ifndef SDDC_PREFETCH
+#define SDDC_PREFETCH 1       // load the next frame's input during the current one
+#endif
 
 // W_32^q = e^{-2 pi i q/32}
 __device__ constexpr float kW32re[32] = {
@@ -120,15 +138,20 @@ __device__ __forceinline__ void load_frame(const int *__restrict__ in32, int blk
 }
 
 template <int D, bool RAND, bool LSB>
-__global__ __launch_bounds__(NT, 2) void r2iq_persistent_kernel(
+__global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
     const int *__restrict__ in32, float2 *__restrict__ out, int nframes,
     const float2 *__restrict__ tw_p1, const float2 *__restrict__ tw_q1,
     const float2 *__restrict__ rec_f, const float2 *__restrict__ rec_i,
+    const float2 *__restrict__ twt_f, const float2 *__restrict__ twt_i,
     const float2 *__restrict__ post8192, const float2 *__restrict__ hsel,
     int tunebin)
 {
     constexpr int N = HALF >> D;
-    __shared__ __attribute__((aligned(16))) float2 lds[HALF];
+    __shared__ __attribute__((aligned(16))) float2 lds[kDB ? 2 * HALF : HALF];
+    // pass-1 twiddle tables, copied once per workgroup: [15][16] forward, [15][S] inverse
+    constexpr int SQ = N >= 512 ? N / 256 : N / 16;
+    __shared__ __attribute__((aligned(16))) float2 twl[15 * 16 + 15 * SQ];
+    float2 *w0 = lds, *w1 = kDB ? lds + HALF : lds;   // this frame's pass buffers
 
     const int tid = (int)threadIdx.x;
     const int G = (int)gridDim.x, w = (int)blockIdx.x;
@@ -147,9 +170,12 @@ __global__ __launch_bounds__(NT, 2) void r2iq_persistent_kernel(
     }
     const float2 pb_ = post8192[(tunebin + tid) & 8191];   // W_8192^{tb + tid}
 
+    for (int i = tid; i < 15 * 16 + 15 * SQ; i += NT)
+        twl[i] = i < 15 * 16 ? tw_p1[i] : tw_q1[i - 15 * 16];   // visible after the first frame's pass-0 barrier
+
     int blk = f0 / FRAMES, k = f0 - blk * FRAMES;
     int x[16];
-    load_frame(in32, blk, k, x);
+    if (SDDC_PREFETCH) load_frame(in32, blk, k, x);
 
     for (int f = f0; f < f1; f++) {
         // Opaque per-iteration copies of the thread index and table pointers: without
@@ -159,6 +185,7 @@ __global__ __launch_bounds__(NT, 2) void r2iq_persistent_kernel(
         asm volatile("" : "+s"(z));
         const int t = tid + z;
         const float2 *tp1 = tw_p1 + z, *tq1 = tw_q1 + z, *hs = hsel + z, *pst = post8192 + z;
+        const float2 *ttf = twt_f + z, *tti = twt_i + z;
         float2 fw1 = fw1_, fw4 = fw4_, iw1 = iw1_, iw4 = iw4_, pb = pb_;
         asm volatile("" : "+v"(fw1), "+v"(fw4), "+v"(iw1), "+v"(iw4), "+v"(pb));
         const int sT = swz(t);            // swz(t + 256 r) = sT + 256 r
@@ -168,6 +195,7 @@ __global__ __launch_bounds__(NT, 2) void r2iq_persistent_kernel(
         // ---- forward pass 0 (R16, NS1): convert + DFT16 from registers ----
         float2 v[16];
         {
+            if (!SDDC_PREFETCH) load_frame(in32, blk, k, x);
             float2 a[16];
 #pragma unroll
             for (int r = 0; r < 16; r++)
@@ -176,40 +204,46 @@ __global__ __launch_bounds__(NT, 2) void r2iq_persistent_kernel(
                 k = 0;
                 ++blk;
             }
-            if (f + 1 < f1) load_frame(in32, blk, k, x);   // prefetch the next frame
+            if (SDDC_PREFETCH && f + 1 < f1) load_frame(in32, blk, k, x);   // prefetch the next frame
             dft16<-1>(a, v);
         }
-        __syncthreads();   // the previous frame's last LDS reads are done
+        if constexpr (!kDB) __syncthreads();   // the previous frame's last LDS reads are done
 #pragma unroll
-        for (int r = 0; r < 16; r++) lds[16 * t + (r ^ x15)] = v[r];          // swz(16t + r)
+        for (int r = 0; r < 16; r++) w0[16 * t + (r ^ x15)] = v[r];          // swz(16t + r)
         __syncthreads();
         // ---- forward pass 1 (R16, NS16): table twiddles W_256^{(t%16) r} ----
         {
             float2 a[16];
 #pragma unroll
-            for (int r = 0; r < 16; r++) a[r] = lds[sT + NT * r];
+            for (int r = 0; r < 16; r++) a[r] = w0[sT + NT * r];
 #pragma unroll
-            for (int r = 1; r < 16; r++) a[r] = cmul(a[r], tp1[(r - 1) * 16 + x15]);
+            for (int r = 1; r < 16; r++)
+                a[r] = cmul(a[r], (SDDC_FAKE & 2) ? make_float2(0.7f, 0.01f * (r + x15)) : twl[(r - 1) * 16 + x15]);
             dft16<-1>(a, v);
         }
-        __syncthreads();
+        if constexpr (!kDB) __syncthreads();
         {
             const int b1 = (t >> 4) * 256;                                     // swz(b1 + x15 + 16 r)
 #pragma unroll
-            for (int r = 0; r < 16; r++) lds[b1 + 16 * r + (x15 ^ r)] = v[r];
+            for (int r = 0; r < 16; r++) w1[b1 + 16 * r + (x15 ^ r)] = v[r];
         }
         __syncthreads();
         // ---- forward pass 2 (R16, NS256): recurrence twiddles W_4096^{t r} ----
         {
             float2 a[16];
 #pragma unroll
-            for (int r = 0; r < 16; r++) a[r] = lds[sT + NT * r];
-            twiddle_rec16<-1>(a, fw1, fw4);
+            for (int r = 0; r < 16; r++) a[r] = w1[sT + NT * r];
+            if constexpr (SDDC_TWTAB) {
+#pragma unroll
+                for (int r = 1; r < 16; r++) a[r] = cmul(a[r], ttf[(r - 1) * NT + t]);
+            } else {
+                twiddle_rec16<-1>(a, fw1, fw4);
+            }
             dft16<-1>(a, v);
         }
-        __syncthreads();
+        if constexpr (!kDB) __syncthreads();
 #pragma unroll
-        for (int r = 0; r < 16; r++) lds[sT + NT * r] = v[r];   // Z, natural order
+        for (int r = 0; r < 16; r++) w0[sT + NT * r] = v[r];   // Z, natural order
         __syncthreads();
 
         if constexpr (N >= 512) {
@@ -229,23 +263,24 @@ __global__ __launch_bounds__(NT, 2) void r2iq_persistent_kernel(
                     const int q = (r - (wrap ? N / NT : 0)) & 31;       // W_8192^{256 r - N wrap}
                     // branch-free: read a clamped (valid) address, zero the result if out of range
                     const bool ok = (unsigned)bin < (unsigned)HALF;
-                    const float2 zk = lds[(sb0 + sh) & (HALF - 1)];
-                    const float2 zc = lds[(sc0 - sh) & (HALF - 1)];
+                    const float2 zk = w0[(sb0 + sh) & (HALF - 1)];
+                    const float2 zc = w0[(sc0 - sh) & (HALF - 1)];
                     const float2 A = make_float2(zk.x + zc.x, zk.y - zc.y);
                     const float2 Bi = make_float2(zk.y + zc.y, zc.x - zk.x);   // (Zk - conj Zc)/i
                     const float2 wb = cmul(pb, make_float2(kW32re[q], kW32im[q]));
-                    const float2 val = cmul(cadd(A, cmul(Bi, wb)), hs[t + NT * r]);
+                    const float2 hv = (SDDC_FAKE & 1) ? make_float2(0.5f, 0.25f * r) : hs[t + NT * r];
+                    const float2 val = cmul(cadd(A, cmul(Bi, wb)), hv);
                     a[r] = ok ? val : make_float2(0.f, 0.f);
                 }
                 dft<R0, +1>(a, u);
             }
-            __syncthreads();
+            if constexpr (!kDB) __syncthreads();
             if constexpr (R0 == 16) {
 #pragma unroll
-                for (int r = 0; r < 16; r++) lds[16 * t + (r ^ x15)] = u[r];
+                for (int r = 0; r < 16; r++) w1[16 * t + (r ^ x15)] = u[r];
             } else {
 #pragma unroll
-                for (int r = 0; r < R0; r++) lds[swz(R0 * t + r)] = u[r];
+                for (int r = 0; r < R0; r++) w1[swz(R0 * t + r)] = u[r];
             }
             __syncthreads();
             // ---- inverse pass 1 (R16, NS = R0): table twiddles W_{16 R0}^{(j%R0) r} ----
@@ -255,25 +290,26 @@ __global__ __launch_bounds__(NT, 2) void r2iq_persistent_kernel(
                 float2 a[16];
                 if constexpr (NB == NT) {
 #pragma unroll
-                    for (int r = 0; r < 16; r++) a[r] = lds[sT + NT * r];
+                    for (int r = 0; r < 16; r++) a[r] = w1[sT + NT * r];
                 } else {
 #pragma unroll
-                    for (int r = 0; r < 16; r++) a[r] = lds[swz(t + NB * r)];
+                    for (int r = 0; r < 16; r++) a[r] = w1[swz(t + NB * r)];
                 }
 #pragma unroll
-                for (int r = 1; r < 16; r++) a[r] = cmulc(a[r], tq1[(r - 1) * R0 + (t % R0)]);
+                for (int r = 1; r < 16; r++)
+                    a[r] = cmulc(a[r], (SDDC_FAKE & 2) ? make_float2(0.7f, 0.01f * (r + t % R0)) : twl[15 * 16 + (r - 1) * R0 + (t % R0)]);
                 dft16<+1>(a, u);
             }
-            __syncthreads();
+            if constexpr (!kDB) __syncthreads();
             if (act) {
                 if constexpr (R0 == 16) {
                     const int b1 = (t >> 4) * 256;
 #pragma unroll
-                    for (int r = 0; r < 16; r++) lds[b1 + 16 * r + (x15 ^ r)] = u[r];
+                    for (int r = 0; r < 16; r++) w0[b1 + 16 * r + (x15 ^ r)] = u[r];
                 } else {
                     const int base = (t / R0) * (16 * R0) + (t % R0);
 #pragma unroll
-                    for (int r = 0; r < 16; r++) lds[swz(base + R0 * r)] = u[r];
+                    for (int r = 0; r < 16; r++) w0[swz(base + R0 * r)] = u[r];
                 }
             }
             __syncthreads();
@@ -282,12 +318,17 @@ __global__ __launch_bounds__(NT, 2) void r2iq_persistent_kernel(
                 float2 a[16];
                 if constexpr (NB == NT) {
 #pragma unroll
-                    for (int r = 0; r < 16; r++) a[r] = lds[sT + NT * r];
+                    for (int r = 0; r < 16; r++) a[r] = w0[sT + NT * r];
                 } else {
 #pragma unroll
-                    for (int r = 0; r < 16; r++) a[r] = lds[swz(t + NB * r)];
+                    for (int r = 0; r < 16; r++) a[r] = w0[swz(t + NB * r)];
                 }
-                twiddle_rec16<+1>(a, iw1, iw4);
+                if constexpr (SDDC_TWTAB) {
+#pragma unroll
+                    for (int r = 1; r < 16; r++) a[r] = cmulc(a[r], (N == HALF ? ttf : tti)[(r - 1) * NB + t]);
+                } else {
+                    twiddle_rec16<+1>(a, iw1, iw4);
+                }
                 dft16<+1>(a, u);
                 if (kc == 0) {
 #pragma unroll
@@ -304,31 +345,31 @@ __global__ __launch_bounds__(NT, 2) void r2iq_persistent_kernel(
             if (t < N) {
                 const int m = t;
                 const int bin = tunebin + m - (m >= N / 2 ? N : 0);
-                tv = split_bin(lds, bin, pst[bin & 8191], hs[m]);
+                tv = split_bin(w0, bin, pst[bin & 8191], hs[m]);
             }
-            __syncthreads();
-            if (t < N) lds[swz(t)] = tv;
+            if constexpr (!kDB) __syncthreads();
+            if (t < N) w1[swz(t)] = tv;
             __syncthreads();
             float2 u[16];
             if (t < 16) {
                 float2 a[R0];
 #pragma unroll
-                for (int r = 0; r < R0; r++) a[r] = lds[swz(t + 16 * r)];
+                for (int r = 0; r < R0; r++) a[r] = w1[swz(t + 16 * r)];
                 dft<R0, +1>(a, u);
             }
-            __syncthreads();
+            if constexpr (!kDB) __syncthreads();
             if (t < 16) {
 #pragma unroll
-                for (int r = 0; r < R0; r++) lds[swz(R0 * t + r)] = u[r];
+                for (int r = 0; r < R0; r++) w0[swz(R0 * t + r)] = u[r];
             }
             __syncthreads();
             constexpr int NB = N / 16;   // = R0
             if (t < NB) {
                 float2 a[16];
 #pragma unroll
-                for (int r = 0; r < 16; r++) a[r] = lds[swz(t + NB * r)];
+                for (int r = 0; r < 16; r++) a[r] = w0[swz(t + NB * r)];
 #pragma unroll
-                for (int r = 1; r < 16; r++) a[r] = cmulc(a[r], tq1[(r - 1) * NB + t]);
+                for (int r = 1; r < 16; r++) a[r] = cmulc(a[r], twl[15 * 16 + (r - 1) * NB + t]);
                 dft16<+1>(a, u);
                 if (kc == 0) {
 #pragma unroll
@@ -338,6 +379,11 @@ __global__ __launch_bounds__(NT, 2) void r2iq_persistent_kernel(
                     for (int r = 0; r < 12; r++) emit<N, LSB>(out_blk, kc, t + NB * r, u[r]);
                 }
             }
+        }
+        if constexpr (kDB) {   // the next frame writes the buffer this frame's last pass did not read
+            float2 *tmp = w0;
+            w0 = w1;
+            w1 = tmp;
         }
     }
 }
@@ -366,7 +412,7 @@ hipError_t launch_v(const KernelTables &t, const int16_t *d_in, int nblk, float 
     if (grid > nframes) grid = nframes;
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), 0, s, reinterpret_cast<const int *>(d_in),
                        reinterpret_cast<float2 *>(d_out), nframes, t.tw_p1, t.tw_q1[D], t.rec_f, t.rec_i[D],
-                       t.post8192, t.hsel[D], tunebin);
+                       t.twt_f, t.twt_i[D], t.post8192, t.hsel[D], tunebin);
     return hipGetLastError();
 }
 

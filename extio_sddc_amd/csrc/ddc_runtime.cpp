@@ -168,7 +168,10 @@ int sddc_ddc_create(float gain, int device, sddc_ddc_t **out)
         host[o_recf + j] = W(j, 4096);
         host[o_recf + 256 + j] = W(4.0 * j, 4096);
     }
-    size_t o_hsel[SDDC_DDC_NDEC], o_q1[SDDC_DDC_NDEC], o_reci[SDDC_DDC_NDEC];
+    const size_t o_twtf = put(15 * 256);
+    for (int r = 1; r < 16; r++)
+        for (int j = 0; j < 256; j++) host[o_twtf + (r - 1) * 256 + j] = W((double)j * r, 4096);
+    size_t o_hsel[SDDC_DDC_NDEC], o_q1[SDDC_DDC_NDEC], o_reci[SDDC_DDC_NDEC], o_twti[SDDC_DDC_NDEC];
     std::vector<std::complex<double>> H(SDDC_DDC_HALF_FFT);
     for (int d = 0; d < SDDC_DDC_NDEC; d++) {
         const int mfft = SDDC_DDC_HALF_FFT >> d;
@@ -187,11 +190,15 @@ int sddc_ddc_create(float gain, int device, sddc_ddc_t **out)
             for (int s = 0; s < S; s++) host[o_q1[d] + (r - 1) * S + s] = W((double)s * r, 16.0 * S);
         // inverse pass-2 recurrence bases W_N^j, W_N^{4j}, j < N/16 (mfft >= 512)
         o_reci[d] = put(2 * 256);
-        if (mfft >= 512)
+        o_twti[d] = put(15 * (size_t)(mfft >= 512 ? mfft / 16 : 1));
+        if (mfft >= 512) {
             for (int j = 0; j < mfft / 16; j++) {
                 host[o_reci[d] + j] = W(j, mfft);
                 host[o_reci[d] + 256 + j] = W(4.0 * j, mfft);
             }
+            for (int r = 1; r < 16; r++)
+                for (int j = 0; j < mfft / 16; j++) host[o_twti[d] + (r - 1) * (mfft / 16) + j] = W((double)j * r, mfft);
+        }
     }
     const size_t ntab = host.size();
     hipError_t e = hipMalloc(&h->d_tables, ntab * sizeof(float2));
@@ -206,10 +213,12 @@ int sddc_ddc_create(float gain, int device, sddc_ddc_t **out)
     h->tables.post8192 = T + o_post;
     h->tables.tw_p1 = T + o_p1;
     h->tables.rec_f = T + o_recf;
+    h->tables.twt_f = T + o_twtf;
     for (int d = 0; d < SDDC_DDC_NDEC; d++) {
         h->tables.hsel[d] = T + o_hsel[d];
         h->tables.tw_q1[d] = T + o_q1[d];
         h->tables.rec_i[d] = T + o_reci[d];
+        h->tables.twt_i[d] = T + o_twti[d];
     }
     *out = h;
     return SDDC_OK;
