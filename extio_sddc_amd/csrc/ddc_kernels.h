@@ -22,6 +22,8 @@ struct KernelTables {
     const float2 *rec_i[7] = {};       // [2][256]: W_N^{j}, W_N^{4j}        inverse pass 2 (N >= 512)
     const float2 *twt_f = nullptr;     // [15][256]: W_4096^{j r}   forward pass 2 twiddles (table form)
     const float2 *twt_i[7] = {};       // [15][N/16]: W_N^{j r}     inverse pass 2 twiddles (N >= 512)
+    const float *rsel[7] = {};         // per d: R_d[k(m)]/2, real amplitude of H_d in inverse-input order
+    const float2 *uph = nullptr;       // [256]: W_4096^{3583 j}, the linear phase of H_d per thread
 };
 
 // v1: one workgroup per frame (kept as a reference variant for A/B timing)

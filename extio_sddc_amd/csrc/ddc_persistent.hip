@@ -44,6 +44,12 @@ constexpr bool kDB = SDDC_DB != 0;
 #ifndef SDDC_FAKE
 #define SDDC_FAKE 0           // timing-only builds: 1 = no hsel loads, 2 = no tp1/tq1 loads, 3 = neither
 #endif
+#ifndef SDDC_HREG
+#define SDDC_HREG 0           // N >= 512: filter as per-thread registers (real R_d x linear phase)
+#endif
+#ifndef SDDC_ZSKIP
+#define SDDC_ZSKIP 0          // skip the split x filter for r whose bins are zero-filled for every thread
+#endif
 #ifndef SDDC_PREFETCH
 #define SDDC_PREFETCH 1       // load the next frame's input during the current one
 #endif
@@ -144,7 +150,8 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
     const float2 *__restrict__ rec_f, const float2 *__restrict__ rec_i,
     const float2 *__restrict__ twt_f, const float2 *__restrict__ twt_i,
     const float2 *__restrict__ post8192, const float2 *__restrict__ hsel,
-    int tunebin)
+    const float *__restrict__ rsel, const float2 *__restrict__ uph,
+    int tunebin, unsigned zmask)
 {
     constexpr int N = HALF >> D;
     __shared__ __attribute__((aligned(16))) float2 lds[kDB ? 2 * HALF : HALF];
@@ -169,6 +176,18 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
         }
     }
     const float2 pb_ = post8192[(tunebin + tid) & 8191];   // W_8192^{tb + tid}
+    // Filter kept in registers (N >= 512): H_d[k] = W_4096^{3583 k} R_d[k] with R_d real, because
+    // the 1025 time-reversed taps at ht[3071..4095] are symmetric about 3583 (fft_mt_r2iq.cpp:200-203).
+    // Thread t needs k = t + 256 r (+ 4096 - N when wrapped): R_d per r, phase W^{3583 t} x constants.
+    constexpr int R0H = N >= 512 ? N / 256 : 1;
+    float hr[R0H];
+    float2 u_ = make_float2(1.f, 0.f), v_ = make_float2(1.f, 0.f);
+    if constexpr (SDDC_HREG && N >= 512) {
+#pragma unroll
+        for (int r = 0; r < R0H; r++) hr[r] = rsel[tid + NT * r];
+        u_ = uph[tid];                 // W_4096^{3583 t}
+        v_ = cmul(pb_, u_);
+    }
 
     for (int i = tid; i < 15 * 16 + 15 * SQ; i += NT)
         twl[i] = i < 15 * 16 ? tw_p1[i] : tw_q1[i - 15 * 16];   // visible after the first frame's pass-0 barrier
@@ -186,8 +205,8 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
         const int t = tid + z;
         const float2 *tp1 = tw_p1 + z, *tq1 = tw_q1 + z, *hs = hsel + z, *pst = post8192 + z;
         const float2 *ttf = twt_f + z, *tti = twt_i + z;
-        float2 fw1 = fw1_, fw4 = fw4_, iw1 = iw1_, iw4 = iw4_, pb = pb_;
-        asm volatile("" : "+v"(fw1), "+v"(fw4), "+v"(iw1), "+v"(iw4), "+v"(pb));
+        float2 fw1 = fw1_, fw4 = fw4_, iw1 = iw1_, iw4 = iw4_, pb = pb_, uu = u_, vv = v_;
+        asm volatile("" : "+v"(fw1), "+v"(fw4), "+v"(iw1), "+v"(iw4), "+v"(pb), "+v"(uu), "+v"(vv));
         const int sT = swz(t);            // swz(t + 256 r) = sT + 256 r
         const int x15 = t & 15;
         float2 *out_blk = out + (size_t)blk * 8 * N;
@@ -262,14 +281,31 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
                     const int bin = b0 + sh;
                     const int q = (r - (wrap ? N / NT : 0)) & 31;       // W_8192^{256 r - N wrap}
                     // branch-free: read a clamped (valid) address, zero the result if out of range
+                    if (SDDC_ZSKIP && ((zmask >> r) & 1)) {   // wave-uniform: whole range zero-filled
+                        a[r] = make_float2(0.f, 0.f);
+                        continue;
+                    }
                     const bool ok = (unsigned)bin < (unsigned)HALF;
                     const float2 zk = w0[(sb0 + sh) & (HALF - 1)];
                     const float2 zc = w0[(sc0 - sh) & (HALF - 1)];
                     const float2 A = make_float2(zk.x + zc.x, zk.y - zc.y);
                     const float2 Bi = make_float2(zk.y + zc.y, zc.x - zk.x);   // (Zk - conj Zc)/i
-                    const float2 wb = cmul(pb, make_float2(kW32re[q], kW32im[q]));
-                    const float2 hv = (SDDC_FAKE & 1) ? make_float2(0.5f, 0.25f * r) : hs[t + NT * r];
-                    const float2 val = cmul(cadd(A, cmul(Bi, wb)), hv);
+                    float2 val;
+                    if constexpr (SDDC_HREG) {
+                        // T = R/2 [A W^{3583k} + Bi W_8192^{bin} W^{3583k}]; both phases are a
+                        // per-thread base (uu, vv) times a compile-time W_32 power
+                        const int eE = (3840 * r + (wrap ? 3583 * (HALF - N) : 0)) & (HALF - 1);
+                        const int qE = (eE / 128) & 31;
+                        const int qF = ((NT * r - (wrap ? N : 0)) / 256 + 2 * eE / 256) & 31;
+                        const float2 ue = cmul(uu, make_float2(kW32re[qE], kW32im[qE]));
+                        const float2 vf = cmul(vv, make_float2(kW32re[qF], kW32im[qF]));
+                        const float2 y = cadd(cmul(A, ue), cmul(Bi, vf));
+                        val = make_float2(y.x * hr[r], y.y * hr[r]);
+                    } else {
+                        const float2 wb = cmul(pb, make_float2(kW32re[q], kW32im[q]));
+                        const float2 hv = (SDDC_FAKE & 1) ? make_float2(0.5f, 0.25f * r) : hs[t + NT * r];
+                        val = cmul(cadd(A, cmul(Bi, wb)), hv);
+                    }
                     a[r] = ok ? val : make_float2(0.f, 0.f);
                 }
                 dft<R0, +1>(a, u);
@@ -388,6 +424,19 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
     }
 }
 
+// Bit r set: for inverse pass-0 leg r every thread's bin tb + t + 256 r (- N if wrapped) lies
+// outside [0, 4096), i.e. the reference zero-fills the whole leg (impl.hpp:91-92, 95-96).
+unsigned zero_bins_mask(int N, int tunebin)
+{
+    unsigned m = 0;
+    if (N < 512) return 0;
+    for (int r = 0; r < N / 256; r++) {
+        const int lo = tunebin + NT * r - (NT * r >= N / 2 ? N : 0);
+        if (lo + NT - 1 < 0 || lo >= HALF) m |= 1u << r;
+    }
+    return m;
+}
+
 int g_occupancy[7][4] = {};
 int g_cus = 0;
 
@@ -412,7 +461,8 @@ hipError_t launch_v(const KernelTables &t, const int16_t *d_in, int nblk, float 
     if (grid > nframes) grid = nframes;
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), 0, s, reinterpret_cast<const int *>(d_in),
                        reinterpret_cast<float2 *>(d_out), nframes, t.tw_p1, t.tw_q1[D], t.rec_f, t.rec_i[D],
-                       t.twt_f, t.twt_i[D], t.post8192, t.hsel[D], tunebin);
+                       t.twt_f, t.twt_i[D], t.post8192, t.hsel[D], t.rsel[D], t.uph, tunebin,
+                       zero_bins_mask(HALF >> D, tunebin));
     return hipGetLastError();
 }
 

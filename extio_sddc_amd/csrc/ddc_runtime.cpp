@@ -172,6 +172,9 @@ int sddc_ddc_create(float gain, int device, sddc_ddc_t **out)
     for (int r = 1; r < 16; r++)
         for (int j = 0; j < 256; j++) host[o_twtf + (r - 1) * 256 + j] = W((double)j * r, 4096);
     size_t o_hsel[SDDC_DDC_NDEC], o_q1[SDDC_DDC_NDEC], o_reci[SDDC_DDC_NDEC], o_twti[SDDC_DDC_NDEC];
+    size_t o_rsel[SDDC_DDC_NDEC];
+    const size_t o_uph = put(256);
+    for (int j = 0; j < 256; j++) host[o_uph + j] = W(3583.0 * j, 4096);
     std::vector<std::complex<double>> H(SDDC_DDC_HALF_FFT);
     for (int d = 0; d < SDDC_DDC_NDEC; d++) {
         const int mfft = SDDC_DDC_HALF_FFT >> d;
@@ -182,6 +185,15 @@ int sddc_ddc_create(float gain, int device, sddc_ddc_t **out)
             // (impl.hpp:90,94 with filter2 = filter + halfFft - mfft/2, impl.hpp:7)
             const std::complex<double> v = H[m < mfft / 2 ? m : SDDC_DDC_HALF_FFT - mfft + m];
             host[o_hsel[d] + m] = make_float2((float)(0.5 * v.real()), (float)(0.5 * v.imag()));
+        }
+        // real amplitude R_d[k] = H_d[k] W^{-3583 k} (the taps are symmetric, so H_d has linear
+        // phase); two floats per float2 slot
+        o_rsel[d] = put((mfft + 1) / 2);
+        for (int m = 0; m < mfft; m++) {
+            const int kk = m < mfft / 2 ? m : SDDC_DDC_HALF_FFT - mfft + m;
+            const double a = 2.0 * M_PI * 3583.0 * kk / 4096.0;
+            const double R = H[kk].real() * std::cos(a) - H[kk].imag() * std::sin(a);
+            reinterpret_cast<float *>(&host[o_rsel[d]])[m] = (float)(0.5 * R);
         }
         // inverse pass-1 table W_{16S}^{s r}, S = mfft/256 (mfft >= 512) or mfft/16
         const int S = mfft >= 512 ? mfft / 256 : mfft / 16;
@@ -214,11 +226,13 @@ int sddc_ddc_create(float gain, int device, sddc_ddc_t **out)
     h->tables.tw_p1 = T + o_p1;
     h->tables.rec_f = T + o_recf;
     h->tables.twt_f = T + o_twtf;
+    h->tables.uph = T + o_uph;
     for (int d = 0; d < SDDC_DDC_NDEC; d++) {
         h->tables.hsel[d] = T + o_hsel[d];
         h->tables.tw_q1[d] = T + o_q1[d];
         h->tables.rec_i[d] = T + o_reci[d];
         h->tables.twt_i[d] = T + o_twti[d];
+        h->tables.rsel[d] = reinterpret_cast<const float *>(T + o_rsel[d]);
     }
     *out = h;
     return SDDC_OK;
