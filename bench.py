@@ -205,7 +205,7 @@ def main() -> None:
                    "parallelism": f"time-segments x{world}" if args.mode == "single" else f"channels x{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "r2iq_frame_kernel" if args.mode == "single" else "r2iq_channels_kernel",
+                     "kernel": "r2iq_persistent_kernel" if args.mode == "single" else "r2iq_channels_kernel",
                      "kernel_ms_per_launch": kern_ms,
                      "algorithmic_bytes_per_launch": alg_bytes,
                      "bytes_per_input_sample": algorithmic_bytes_per_sample(d, nch_local)},
