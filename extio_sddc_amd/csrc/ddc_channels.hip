@@ -1,0 +1,269 @@
+// ddc_channels.hip — many-channel DDC for gfx950 (up to 1024
+// tune offsets of one stream, d >= 4 i.e. mfft N <= 256).
+//
+// Work item = (frame, chunk of <= 128 channels).  Per item the workgroup computes the
+// frame's forward transform ONCE (as ddc_persistent.hip: 3 x radix-16 Stockham in 32 KB
+// of swizzled LDS, int16 -> float with optional RAND), then walks the chunk G = 256/TPC
+// channels at a time, TPC = N/16 threads per channel:
+//   pass A  r2c split x filter for the channel's N bins around its tune bin
+//           (Core/fft_mt_r2iq_impl.hpp:76-96), DFT-16 in registers, -> per-channel LDS slice
+//   pass B  radix-(N/16) Stockham step with W_256 twiddles from LDS, overlap-discard
+//           write of the kept outputs to the channel's stream (impl.hpp:117-138)
+// Channel c's output stream starts at out + c * stride (float2 units).  Persistent grid:
+// CUs x resident workgroups, contiguous item ranges.
+#include <hip/hip_runtime.h>
+
+#include "ddc_consts.h"
+#include "ddc_kernels.h"
+#include "fft_device.hpp"
+
+namespace sddc {
+namespace {
+
+constexpr int NT = 256;
+constexpr int HALF = 4096;
+constexpr int HOP = 6144;
+constexpr int BLOCK = 65536;
+constexpr int FRAMES = 11;
+constexpr int CHUNK = 128;    // channels per work item
+
+__device__ __forceinline__ int swz(int e) { return e ^ ((e >> 4) & 15); }
+
+template <bool RAND>
+__device__ __forceinline__ float derand(int v)
+{
+    const float f = (float)v;
+    if constexpr (!RAND) return f;
+    return __int_as_float(__float_as_int(f) ^ (v << 31));   // odd int16 ^ 0xFFFE == -v
+}
+
+template <int DIR>
+__device__ __forceinline__ void twiddle_rec16(float2 *a, float2 w1, float2 w4)
+{
+    if (DIR > 0) {
+        w1.y = -w1.y;
+        w4.y = -w4.y;
+    }
+    const float2 w2 = cmul(w1, w1), w3 = cmul(w2, w1);
+    const float2 w8 = cmul(w4, w4), w12 = cmul(w8, w4);
+    a[1] = cmul(a[1], w1);
+    a[2] = cmul(a[2], w2);
+    a[3] = cmul(a[3], w3);
+    a[4] = cmul(a[4], w4);
+    a[5] = cmul(a[5], cmul(w4, w1));
+    a[6] = cmul(a[6], cmul(w4, w2));
+    a[7] = cmul(a[7], cmul(w4, w3));
+    a[8] = cmul(a[8], w8);
+    a[9] = cmul(a[9], cmul(w8, w1));
+    a[10] = cmul(a[10], cmul(w8, w2));
+    a[11] = cmul(a[11], cmul(w8, w3));
+    a[12] = cmul(a[12], w12);
+    a[13] = cmul(a[13], cmul(w12, w1));
+    a[14] = cmul(a[14], cmul(w12, w2));
+    a[15] = cmul(a[15], cmul(w12, w3));
+}
+
+template <int N>
+__device__ __forceinline__ constexpr float2 wsplit(int r)
+{
+    if constexpr (N == 256) return make_float2(kWsplitRe256[r], kWsplitIm256[r]);
+    else if constexpr (N == 128) return make_float2(kWsplitRe128[r], kWsplitIm128[r]);
+    else return make_float2(kWsplitRe64[r], kWsplitIm64[r]);
+}
+
+template <int D, bool RAND, bool LSB>
+__global__ __launch_bounds__(NT, 2) void r2iq_channels_v2_kernel(
+    const int *__restrict__ in32, float2 *__restrict__ out, size_t stride, int nframes,
+    const int *__restrict__ tunebins, int nch, const float2 *__restrict__ tw_p1,
+    const float2 *__restrict__ rec_f, const float2 *__restrict__ post8192, const float2 *__restrict__ hsel)
+{
+    constexpr int N = HALF >> D;
+    static_assert(N <= 256 && N >= 64, "channels v2 covers d = 4..6");
+    constexpr int TPC = N / 16;          // threads per channel
+    constexpr int G = NT / TPC;          // channels in flight
+    constexpr int RB = N / 16;           // pass-B radix
+    constexpr int BPT = 16 / TPC;        // pass-B butterflies per thread
+
+    __shared__ __attribute__((aligned(16))) float2 zl[HALF];
+    __shared__ __attribute__((aligned(16))) float2 work[G * N];
+    __shared__ __attribute__((aligned(16))) float2 twl[15 * 16];
+    __shared__ __attribute__((aligned(16))) float2 hl[N];
+
+    const int tid = (int)threadIdx.x;
+    const int nchunks = (nch + CHUNK - 1) / CHUNK;
+    const long long items = (long long)nframes * nchunks;
+    const int i0 = (int)(items * blockIdx.x / gridDim.x), i1 = (int)(items * (blockIdx.x + 1) / gridDim.x);
+    if (i0 >= i1) return;
+    for (int i = tid; i < 15 * 16; i += NT) twl[i] = tw_p1[i];
+    for (int i = tid; i < N; i += NT) hl[i] = hsel[i];
+    const float2 fw1_ = rec_f[tid], fw4_ = rec_f[NT + tid];
+    const int l_ = tid % TPC, g_ = tid / TPC;
+
+    for (int it = i0; it < i1; it++) {
+        int z = 0;
+        asm volatile("" : "+s"(z));
+        const int t = tid + z, l = l_ + z, g = g_ + z;
+        float2 fw1 = fw1_, fw4 = fw4_;
+        asm volatile("" : "+v"(fw1), "+v"(fw4));
+        const int f = it / nchunks, chunk = it - f * nchunks;
+        const int blk = f / FRAMES, k = f - blk * FRAMES;
+        const int sT = swz(t), x15 = t & 15;
+        // ---------------- forward: Z = FFT4096(x_even + i x_odd) in zl ----------------
+        float2 v[16];
+        {
+            const int *p = in32 + ((size_t)blk * BLOCK + (size_t)k * HOP) / 2 + t;
+            float2 a[16];
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int w = p[NT * r];
+                a[r] = make_float2(derand<RAND>((int)(short)(w & 0xffff)), derand<RAND>(w >> 16));
+            }
+            dft16<-1>(a, v);
+        }
+        __syncthreads();   // previous item's readers of zl / twl / hl done
+#pragma unroll
+        for (int r = 0; r < 16; r++) zl[16 * t + (r ^ x15)] = v[r];
+        __syncthreads();
+        {
+            float2 a[16];
+#pragma unroll
+            for (int r = 0; r < 16; r++) a[r] = zl[sT + NT * r];
+#pragma unroll
+            for (int r = 1; r < 16; r++) a[r] = cmul(a[r], twl[(r - 1) * 16 + x15]);
+            dft16<-1>(a, v);
+        }
+        __syncthreads();
+        {
+            const int b1 = (t >> 4) * 256;
+#pragma unroll
+            for (int r = 0; r < 16; r++) zl[b1 + 16 * r + (x15 ^ r)] = v[r];
+        }
+        __syncthreads();
+        {
+            float2 a[16];
+#pragma unroll
+            for (int r = 0; r < 16; r++) a[r] = zl[sT + NT * r];
+            twiddle_rec16<-1>(a, fw1, fw4);
+            dft16<-1>(a, v);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < 16; r++) zl[sT + NT * r] = v[r];
+        __syncthreads();
+
+        // ---------------- channels, G at a time ----------------
+        const int cbeg = chunk * CHUNK;
+        const int cend = min(cbeg + CHUNK, nch);
+        float2 *wg = work + g * N;
+        for (int cg = cbeg; cg < cend; cg += G) {
+            const int c = cg + g;
+            const bool cok = c < cend;
+            const int tb = cok ? tunebins[c] : 0;
+            // pass A: bins tb + m (- N), m = l + TPC r; split x filter; DFT-16
+            {
+                const float2 pbc = post8192[(tb + l) & 8191];     // W_8192^{tb + l}
+                float2 a[16];
+#pragma unroll
+                for (int r = 0; r < 16; r++) {
+                    const int m = l + TPC * r;
+                    const bool wrap = TPC * r >= N / 2;
+                    const int bin = tb + m - (wrap ? N : 0);
+                    const bool ok = cok && (unsigned)bin < (unsigned)HALF;
+                    const float2 zk = zl[swz(bin & (HALF - 1))];
+                    const float2 zc = zl[swz((HALF - bin) & (HALF - 1))];
+                    const float2 A = make_float2(zk.x + zc.x, zk.y - zc.y);
+                    const float2 Bi = make_float2(zk.y + zc.y, zc.x - zk.x);   // (Zk - conj Zc)/i
+                    const float2 wb = cmul(pbc, wsplit<N>(r));
+                    const float2 val = cmul(cadd(A, cmul(Bi, wb)), hl[m]);
+                    a[r] = ok ? val : make_float2(0.f, 0.f);
+                }
+                float2 u[16];
+                dft16<+1>(a, u);
+#pragma unroll
+                for (int r = 0; r < 16; r++) wg[swz(16 * l + r)] = u[r];
+            }
+            __syncthreads();
+            // pass B: radix-RB Stockham step (NS = 16), twiddles W_N^{j q} = W_256^{(256/N) j q}
+            if (cok) {
+                float2 *ob = out + (size_t)c * stride + (size_t)blk * 8 * N;
+#pragma unroll
+                for (int b = 0; b < BPT; b++) {
+                    const int j = l + TPC * b;          // butterfly 0..15
+                    float2 a[RB], y[RB];
+#pragma unroll
+                    for (int q = 0; q < RB; q++) a[q] = wg[swz(j + 16 * q)];
+#pragma unroll
+                    for (int q = 1; q < RB; q++) a[q] = cmulc(a[q], twl[((256 / N) * q - 1) * 16 + j]);
+                    dft<RB, +1>(a, y);
+                    // outputs n = j + 16 q; keep y[N/4, 3N/4) for k = 0, y[0, 3N/4) otherwise
+#pragma unroll
+                    for (int q = 0; q < RB; q++) {
+                        const int n = j + 16 * q;
+                        if (16 * q >= 3 * N / 4) continue;
+                        float2 o = y[q];
+                        if constexpr (LSB) o.y = -o.y;
+                        if (k == 0) {
+                            if (16 * q >= N / 4) ob[n - N / 4] = o;
+                        } else {
+                            ob[N / 2 + (3 * N / 4) * (k - 1) + n] = o;
+                        }
+                    }
+                }
+            }
+            __syncthreads();   // wg is rewritten by the next channel group
+        }
+    }
+}
+
+int g_occ[3][4] = {};
+int g_cus = 0;
+
+template <int D, bool RAND, bool LSB>
+hipError_t launch_v(const KernelTables &t, const int16_t *d_in, int nblk, const int *d_tunebins, int nch,
+                    float *d_out, size_t stride_floats, int device, hipStream_t s)
+{
+    auto kern = r2iq_channels_v2_kernel<D, RAND, LSB>;
+    int &occ = g_occ[D - 4][(RAND ? 2 : 0) + (LSB ? 1 : 0)];
+    if (occ == 0) {
+        int nb = 0;
+        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, NT, 0);
+        if (e != hipSuccess) return e;
+        e = hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, device);
+        if (e != hipSuccess) return e;
+        occ = nb > 0 ? nb : 1;
+    }
+    const int nframes = nblk * FRAMES;
+    const long long items = (long long)nframes * ((nch + CHUNK - 1) / CHUNK);
+    const int grid = (int)(items < (long long)g_cus * occ ? items : (long long)g_cus * occ);
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), 0, s, reinterpret_cast<const int *>(d_in),
+                       reinterpret_cast<float2 *>(d_out), stride_floats / 2, nframes, d_tunebins, nch,
+                       t.tw_p1, t.rec_f, t.post8192, t.hsel[D]);
+    return hipGetLastError();
+}
+
+template <int D>
+hipError_t launch_d(const KernelTables &t, const int16_t *d_in, int nblk, const int *d_tunebins, int nch,
+                    float *d_out, size_t stride_floats, int lsb, int rand, int device, hipStream_t s)
+{
+    if (rand)
+        return lsb ? launch_v<D, true, true>(t, d_in, nblk, d_tunebins, nch, d_out, stride_floats, device, s)
+                   : launch_v<D, true, false>(t, d_in, nblk, d_tunebins, nch, d_out, stride_floats, device, s);
+    return lsb ? launch_v<D, false, true>(t, d_in, nblk, d_tunebins, nch, d_out, stride_floats, device, s)
+               : launch_v<D, false, false>(t, d_in, nblk, d_tunebins, nch, d_out, stride_floats, device, s);
+}
+
+}  // namespace
+
+hipError_t launch_channels_v2(const KernelTables &t, int d, const int16_t *d_in, int nblk, const int *d_tunebins,
+                              int nch, float *d_out, size_t stride_floats, int lsb, int rand, int device,
+                              hipStream_t s)
+{
+    switch (d) {
+    case 4: return launch_d<4>(t, d_in, nblk, d_tunebins, nch, d_out, stride_floats, lsb, rand, device, s);
+    case 5: return launch_d<5>(t, d_in, nblk, d_tunebins, nch, d_out, stride_floats, lsb, rand, device, s);
+    case 6: return launch_d<6>(t, d_in, nblk, d_tunebins, nch, d_out, stride_floats, lsb, rand, device, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace sddc

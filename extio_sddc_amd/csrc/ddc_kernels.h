@@ -37,6 +37,11 @@ hipError_t launch_frames_persistent(const KernelTables &t, int d, const int16_t 
 
 int channels_per_group(int d, int nch);
 
+// many-channel v2 (d = 4..6): persistent, forward once per (frame, 128-channel chunk)
+hipError_t launch_channels_v2(const KernelTables &t, int d, const int16_t *d_in, int nblk, const int *d_tunebins,
+                              int nch, float *d_out, size_t stride_floats, int lsb, int rand, int device,
+                              hipStream_t s);
+
 hipError_t launch_channels(const KernelTables &t, int d, const int16_t *d_in, int nblk,
                            const int *d_tunebins, int nch, float *d_out, size_t stride_floats,
                            int lsb, int rand, hipStream_t s);

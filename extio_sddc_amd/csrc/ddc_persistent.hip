@@ -203,7 +203,7 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
         int z = 0;
         asm volatile("" : "+s"(z));
         const int t = tid + z;
-        const float2 *tp1 = tw_p1 + z, *tq1 = tw_q1 + z, *hs = hsel + z, *pst = post8192 + z;
+        const float2 *hs = hsel + z, *pst = post8192 + z;
         const float2 *ttf = twt_f + z, *tti = twt_i + z;
         float2 fw1 = fw1_, fw4 = fw4_, iw1 = iw1_, iw4 = iw4_, pb = pb_, uu = u_, vv = v_;
         asm volatile("" : "+v"(fw1), "+v"(fw4), "+v"(iw1), "+v"(iw4), "+v"(pb), "+v"(uu), "+v"(vv));

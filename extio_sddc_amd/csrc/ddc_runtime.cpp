@@ -372,8 +372,12 @@ int sddc_ddc_process_channels_device(sddc_ddc_t *h, const int16_t *d_in, int nbl
         // synchronous: the host array may go away after we return
         HIP_TRY(hipMemcpy(h->d_tunebins, tunebins, nch * sizeof(int), hipMemcpyHostToDevice));
     }
-    HIP_TRY(sddc::launch_channels(h->tables, h->d, d_in, nblk, h->d_tunebins, nch, d_out,
-                                  out_stride_floats, h->lsb, h->rand, s));
+    if (h->d >= 4 && h->variant == 0)
+        HIP_TRY(sddc::launch_channels_v2(h->tables, h->d, d_in, nblk, h->d_tunebins, nch, d_out,
+                                         out_stride_floats, h->lsb, h->rand, h->device, s));
+    else
+        HIP_TRY(sddc::launch_channels(h->tables, h->d, d_in, nblk, h->d_tunebins, nch, d_out,
+                                      out_stride_floats, h->lsb, h->rand, s));
     return SDDC_OK;
 }
 

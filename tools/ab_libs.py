@@ -23,7 +23,7 @@ def main():
     ap.add_argument("--d", type=int, nargs="+", default=[0, 1, 2, 3, 4])
     ap.add_argument("--nblk", type=int, default=2048)
     ap.add_argument("--rounds", type=int, default=10)
-    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--tunebin", type=int, default=1024)
     args = ap.parse_args()
 
@@ -47,6 +47,14 @@ def main():
     d_in = torch.randint(-32768, 32767, (4096 + nblk * 65536,), dtype=torch.int16, device=dev, generator=g)
     s = torch.cuda.current_stream().cuda_stream
     res = {}
+    # heat the chip for ~2 s so every variant is timed at the sustained (power-limited) clock
+    heat = torch.empty(nblk * 32768 * 2, dtype=torch.float32, device=dev)
+    libs[0].sddc_ddc_set_decimation(handles[0], 0)
+    t_end = __import__("time").time() + 2.0
+    while __import__("time").time() < t_end:
+        libs[0].sddc_ddc_process_device(handles[0], d_in.data_ptr(), nblk, heat.data_ptr(), s)
+        torch.cuda.synchronize()
+    del heat
     for d in args.d:
         n_out = nblk * (32768 >> d) * 2
         outs = [torch.empty(n_out, dtype=torch.float32, device=dev) for _ in libs]

@@ -9,7 +9,8 @@ C=$R/extio_sddc_amd/csrc
 F="-O3 -std=c++17 -fPIC -fno-slp-vectorize -I$C -I$R/include"
 hipcc --offload-arch=gfx950 $F -c $C/ddc_kernels.hip -o $O/k.o
 hipcc --offload-arch=gfx950 $F $EXTRA -c $C/ddc_persistent.hip -o $O/p.o
+hipcc --offload-arch=gfx950 $F $EXTRA -c $C/ddc_channels.hip -o $O/c.o
 hipcc $F -ffp-contract=off -c $C/ddc_runtime.cpp -o $O/r.o
 hipcc $F -ffp-contract=off -c $C/filterbank.cpp -o $O/f.o
-hipcc --offload-arch=gfx950 -shared $O/k.o $O/p.o $O/r.o $O/f.o -o $R/build/ab/$NAME.so
+hipcc --offload-arch=gfx950 -shared $O/k.o $O/p.o $O/c.o $O/r.o $O/f.o -o $R/build/ab/$NAME.so
 echo built $R/build/ab/$NAME.so
