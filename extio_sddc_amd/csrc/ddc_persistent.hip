@@ -42,7 +42,7 @@ constexpr bool kDB = SDDC_DB != 0;
 #define SDDC_TWTAB 0          // NS=N/16 passes: 1 = coalesced [r][t] twiddle table, 0 = register recurrence
 #endif
 #ifndef SDDC_FAKE
-#define SDDC_FAKE 0           // timing-only builds: 1 = no hsel loads, 2 = no tp1/tq1 loads, 3 = neither
+#define SDDC_FAKE 0           // timing-only builds: 1 = no hsel loads, 2 = no tp1/tq1 loads, 4 = no loop barriers
 #endif
 #ifndef SDDC_HREG
 #define SDDC_HREG 0           // N >= 512: filter as per-thread registers (real R_d x linear phase)
@@ -69,6 +69,8 @@ __device__ constexpr float kW32im[32] = {
     3.826834324e-01f, 5.555702330e-01f, 7.071067812e-01f, 8.314696123e-01f, 9.238795325e-01f,
     9.807852804e-01f, 1.0f, 9.807852804e-01f, 9.238795325e-01f, 8.314696123e-01f, 7.071067812e-01f,
     5.555702330e-01f, 3.826834324e-01f, 1.950903220e-01f};
+
+#define LOOP_SYNC() do { if constexpr (!(SDDC_FAKE & 4)) __syncthreads(); } while (0)
 
 __device__ __forceinline__ int swz(int e) { return e ^ ((e >> 4) & 15); }
 
@@ -226,10 +228,10 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
             if (SDDC_PREFETCH && f + 1 < f1) load_frame(in32, blk, k, x);   // prefetch the next frame
             dft16<-1>(a, v);
         }
-        if constexpr (!kDB) __syncthreads();   // the previous frame's last LDS reads are done
+        if constexpr (!kDB) LOOP_SYNC();   // the previous frame's last LDS reads are done
 #pragma unroll
         for (int r = 0; r < 16; r++) w0[16 * t + (r ^ x15)] = v[r];          // swz(16t + r)
-        __syncthreads();
+        LOOP_SYNC();
         // ---- forward pass 1 (R16, NS16): table twiddles W_256^{(t%16) r} ----
         {
             float2 a[16];
@@ -240,13 +242,13 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
                 a[r] = cmul(a[r], (SDDC_FAKE & 2) ? make_float2(0.7f, 0.01f * (r + x15)) : twl[(r - 1) * 16 + x15]);
             dft16<-1>(a, v);
         }
-        if constexpr (!kDB) __syncthreads();
+        if constexpr (!kDB) LOOP_SYNC();
         {
             const int b1 = (t >> 4) * 256;                                     // swz(b1 + x15 + 16 r)
 #pragma unroll
             for (int r = 0; r < 16; r++) w1[b1 + 16 * r + (x15 ^ r)] = v[r];
         }
-        __syncthreads();
+        LOOP_SYNC();
         // ---- forward pass 2 (R16, NS256): recurrence twiddles W_4096^{t r} ----
         {
             float2 a[16];
@@ -260,10 +262,10 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
             }
             dft16<-1>(a, v);
         }
-        if constexpr (!kDB) __syncthreads();
+        if constexpr (!kDB) LOOP_SYNC();
 #pragma unroll
         for (int r = 0; r < 16; r++) w0[sT + NT * r] = v[r];   // Z, natural order
-        __syncthreads();
+        LOOP_SYNC();
 
         if constexpr (N >= 512) {
             constexpr int R0 = N / 256;
@@ -310,7 +312,7 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
                 }
                 dft<R0, +1>(a, u);
             }
-            if constexpr (!kDB) __syncthreads();
+            if constexpr (!kDB) LOOP_SYNC();
             if constexpr (R0 == 16) {
 #pragma unroll
                 for (int r = 0; r < 16; r++) w1[16 * t + (r ^ x15)] = u[r];
@@ -318,7 +320,7 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
 #pragma unroll
                 for (int r = 0; r < R0; r++) w1[swz(R0 * t + r)] = u[r];
             }
-            __syncthreads();
+            LOOP_SYNC();
             // ---- inverse pass 1 (R16, NS = R0): table twiddles W_{16 R0}^{(j%R0) r} ----
             constexpr int NB = N / 16;
             const bool act = (NB == NT) || t < NB;
@@ -336,7 +338,7 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
                     a[r] = cmulc(a[r], (SDDC_FAKE & 2) ? make_float2(0.7f, 0.01f * (r + t % R0)) : twl[15 * 16 + (r - 1) * R0 + (t % R0)]);
                 dft16<+1>(a, u);
             }
-            if constexpr (!kDB) __syncthreads();
+            if constexpr (!kDB) LOOP_SYNC();
             if (act) {
                 if constexpr (R0 == 16) {
                     const int b1 = (t >> 4) * 256;
@@ -348,7 +350,7 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
                     for (int r = 0; r < 16; r++) w0[swz(base + R0 * r)] = u[r];
                 }
             }
-            __syncthreads();
+            LOOP_SYNC();
             // ---- inverse pass 2 (R16, NS = N/16): recurrence twiddles, overlap-discard write ----
             if (act) {
                 float2 a[16];
@@ -383,9 +385,9 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
                 const int bin = tunebin + m - (m >= N / 2 ? N : 0);
                 tv = split_bin(w0, bin, pst[bin & 8191], hs[m]);
             }
-            if constexpr (!kDB) __syncthreads();
+            if constexpr (!kDB) LOOP_SYNC();
             if (t < N) w1[swz(t)] = tv;
-            __syncthreads();
+            LOOP_SYNC();
             float2 u[16];
             if (t < 16) {
                 float2 a[R0];
@@ -393,12 +395,12 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
                 for (int r = 0; r < R0; r++) a[r] = w1[swz(t + 16 * r)];
                 dft<R0, +1>(a, u);
             }
-            if constexpr (!kDB) __syncthreads();
+            if constexpr (!kDB) LOOP_SYNC();
             if (t < 16) {
 #pragma unroll
                 for (int r = 0; r < R0; r++) w0[swz(R0 * t + r)] = u[r];
             }
-            __syncthreads();
+            LOOP_SYNC();
             constexpr int NB = N / 16;   // = R0
             if (t < NB) {
                 float2 a[16];

@@ -6,7 +6,10 @@
 // byte layout of the private fields (randADC @44, sideband @45, Core/r2iq.h).
 //
 //   r2iq_harness IN.bin NBLK D TUNEBIN LSB RAND GAIN OUT.bin
+// OUT.bin "-" discards the IQ and reports the end-to-end input rate (PCIe + host copies
+// included); IN.bin may hold fewer blocks than NBLK, it is then cycled.
 #include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -24,10 +27,17 @@ int main(int argc, char **argv)
     const int nblk = std::atoi(argv[2]), d = std::atoi(argv[3]), tb = std::atoi(argv[4]);
     const bool lsb = std::atoi(argv[5]) != 0, rnd = std::atoi(argv[6]) != 0;
     const float gain = (float)std::atof(argv[7]);
-    std::vector<int16_t> data((size_t)nblk * 65536);
     FILE *in = std::fopen(argv[1], "rb");
-    if (!in || fread(data.data(), sizeof(int16_t), data.size(), in) != data.size()) return 2;
+    if (!in) return 2;
+    std::fseek(in, 0, SEEK_END);
+    const long bytes = std::ftell(in);
+    std::fseek(in, 0, SEEK_SET);
+    const int have = (int)(bytes / (65536 * 2));
+    if (have < 1) return 2;
+    std::vector<int16_t> data((size_t)have * 65536);
+    if (fread(data.data(), sizeof(int16_t), data.size(), in) != data.size()) return 2;
     std::fclose(in);
+    const bool discard = std::strcmp(argv[8], "-") == 0;
 
     ringbuffer<int16_t> inbuf;           // 64 slots, like RadioHandlerClass::inputbuffer
     ringbuffer<float> outbuf;
@@ -55,20 +65,24 @@ int main(int argc, char **argv)
         for (int b = 0; b < nblk; b++) {
             int16_t *p = inbuf.getWritePtr();
             if (!base->IsOn()) return;
-            std::memcpy(p, data.data() + (size_t)b * 65536, 65536 * sizeof(int16_t));
+            std::memcpy(p, data.data() + (size_t)(b % have) * 65536, 65536 * sizeof(int16_t));
             inbuf.WriteDone();
         }
     });
-    FILE *out = std::fopen(argv[8], "wb");
+    FILE *out = discard ? nullptr : std::fopen(argv[8], "wb");
     const int want = nblk >> d;
     int got = 0;
+    const auto t0 = std::chrono::steady_clock::now();
     for (; got < want; got++) {
         const float *p = outbuf.getReadPtr();
         if (!base->IsOn()) break;
-        fwrite(p, sizeof(float), 65536, out);
+        if (out) fwrite(p, sizeof(float), 65536, out);
         outbuf.ReadDone();
     }
-    std::fclose(out);
+    const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (out) std::fclose(out);
+    if (discard)
+        std::printf("end-to-end: %d blocks in %.3f s = %.1f input MS/s\n", nblk, secs, nblk * 65536.0 / secs / 1e6);
     base->TurnOff();
     producer.join();
     std::printf("output blocks %d of %d, residual fc %g, gpu blocks %llu\n", got, want, fc,
