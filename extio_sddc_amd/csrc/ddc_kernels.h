@@ -22,18 +22,18 @@ struct KernelTables {
     const float2 *rec_i[7] = {};       // [2][256]: W_N^{j}, W_N^{4j}        inverse pass 2 (N >= 512)
     const float2 *twt_f = nullptr;     // [15][256]: W_4096^{j r}   forward pass 2 twiddles (table form)
     const float2 *twt_i[7] = {};       // [15][N/16]: W_N^{j r}     inverse pass 2 twiddles (N >= 512)
-    const float *rsel[7] = {};         // per d: R_d[k(m)]/2, real amplitude of H_d in inverse-input order
-    const float2 *uph = nullptr;       // [256]: W_4096^{3583 j}, the linear phase of H_d per thread
 };
 
 // v1: one workgroup per frame (kept as a reference variant for A/B timing)
 hipError_t launch_frames(const KernelTables &t, int d, const int16_t *d_in, int nblk, float *d_out,
                          int tunebin, int lsb, int rand, hipStream_t s);
 
-// v2 (default): persistent workgroups, input prefetch, swizzled LDS
+// v2 (default): persistent workgroups, input prefetch, swizzled LDS.  pq: the split x filter
+// coefficients of (d, tunebin), HALF >> d float4, built by launch_build_split_filter.
 hipError_t launch_frames_persistent(const KernelTables &t, int d, const int16_t *d_in, int nblk,
-                                    float *d_out, int tunebin, int lsb, int rand, int device,
-                                    hipStream_t s);
+                                    float *d_out, const float4 *pq, int tunebin, int lsb, int rand,
+                                    int device, hipStream_t s);
+hipError_t launch_build_split_filter(const KernelTables &t, int d, int tunebin, float4 *pq, hipStream_t s);
 
 int channels_per_group(int d, int nch);
 

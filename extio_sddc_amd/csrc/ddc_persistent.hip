@@ -44,11 +44,11 @@ constexpr bool kDB = SDDC_DB != 0;
 #ifndef SDDC_FAKE
 #define SDDC_FAKE 0           // timing-only builds: 1 = no hsel loads, 2 = no tp1/tq1 loads, 4 = no loop barriers
 #endif
-#ifndef SDDC_HREG
-#define SDDC_HREG 0           // N >= 512: filter as per-thread registers (real R_d x linear phase)
+#ifndef SDDC_PQ
+#define SDDC_PQ 1             // split x filter from the per-(d, tunebin) coefficient table (P, Q)
 #endif
-#ifndef SDDC_ZSKIP
-#define SDDC_ZSKIP 0          // skip the split x filter for r whose bins are zero-filled for every thread
+#ifndef SDDC_BUF
+#define SDDC_BUF 1            // buffer loads/stores (SGPR base + offsets, no per-access VALU address math)
 #endif
 #ifndef SDDC_PREFETCH
 #define SDDC_PREFETCH 1       // load the next frame's input during the current one
@@ -118,6 +118,18 @@ __device__ __forceinline__ void twiddle_rec16(float2 *a, float2 w1, float2 w4)
 
 // X[bin] * Hh[m] from Z in LDS (Hh = H/2): the r2c split E + W^bin O, times the filter.
 // Zero for bins the reference zero-fills (impl.hpp:91-92, 95-96).
+//   X Hh = Hh [(Zk + conj Zc) - i W^bin (Zk - conj Zc)] = Zk P + conj(Zc) Q,
+//   P = Hh (1 - i W^bin),  Q = Hh (1 + i W^bin)     (Zc = Z[(4096 - bin) mod 4096])
+// split_pq evaluates the right-hand form from the table built by build_split_filter_kernel,
+// whose entries are zero for out-of-band bins; split_bin is the direct form (SDDC_PQ=0).
+__device__ __forceinline__ float2 split_pq(float2 zk, float2 zc, float4 c)
+{
+    float2 v;
+    v.x = zk.x * c.x - zk.y * c.y + zc.x * c.z + zc.y * c.w;
+    v.y = zk.x * c.y + zk.y * c.x + zc.x * c.w - zc.y * c.z;
+    return v;
+}
+
 __device__ __forceinline__ float2 split_bin(const float2 *lds, int bin, float2 wbin, float2 hh)
 {
     if (bin < 0 || bin >= HALF) return make_float2(0.f, 0.f);
@@ -126,6 +138,40 @@ __device__ __forceinline__ float2 split_bin(const float2 *lds, int bin, float2 w
     const float2 A = make_float2(zk.x + zc.x, zk.y - zc.y);
     const float2 Bi = make_float2(zk.y + zc.y, zc.x - zk.x);   // (Zk - conj Zc) / i
     return cmul(cadd(A, cmul(Bi, wbin)), hh);
+}
+
+// Raw buffer access: a wave-uniform base (SGPRs), a per-thread byte offset and a uniform
+// byte offset (SGPR or immediate), so per-access address arithmetic is scalar.
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void *base)
+{
+    // raw (stride 0) buffer, byte range checked against 2^31 - 1; dword3 for gfx950
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ float4 buf_load16(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff)
+{
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
+    return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+}
+__device__ __forceinline__ int buf_load4(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff)
+{
+    return (int)__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0);
+}
+__device__ __forceinline__ void buf_store8(float2 v, __amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff)
+{
+    u32x2 u;
+    u.x = __float_as_uint(v.x);
+    u.y = __float_as_uint(v.y);
+    __builtin_amdgcn_raw_buffer_store_b64(u, r, voff, soff, 0);
+}
+
+// Frame k of a block: output base of the kept samples, relative to the block's output
+template <int N>
+__device__ __forceinline__ int emit_base(int k)
+{
+    return k == 0 ? -N / 4 : N / 2 + (3 * N / 4) * (k - 1);
 }
 
 template <int N, bool LSB>
@@ -138,8 +184,41 @@ __device__ __forceinline__ void emit(float2 *__restrict__ out_blk, int k, int n,
         out_blk[N / 2 + (3 * N / 4) * (k - 1) + n] = v;
 }
 
+// The kept outputs n = t + NB r of frame k (r in [4, 12) for k = 0, [0, 12) otherwise)
+template <int N, int NB, bool LSB>
+__device__ __forceinline__ void emit_frame(float2 *__restrict__ out_blk, int k, int t, const float2 (&u)[16])
+{
+    if constexpr (SDDC_BUF) {
+        const __amdgpu_buffer_rsrc_t ro = buf_rsrc(out_blk + emit_base<N>(k));
+        const unsigned vo = 8u * (unsigned)t;
+        const int r0 = k == 0 ? 4 : 0;   // wave-uniform
+#pragma unroll
+        for (int r = 0; r < 12; r++) {
+            if (r < r0) continue;
+            float2 v = u[r];
+            if constexpr (LSB) v.y = -v.y;   // copy<flip=true>, fft_mt_r2iq.h:63-71
+            buf_store8(v, ro, vo, 8u * NB * r);
+        }
+        return;
+    }
+    if (k == 0) {
+#pragma unroll
+        for (int r = 4; r < 12; r++) emit<N, LSB>(out_blk, 0, t + NB * r, u[r]);
+    } else {
+#pragma unroll
+        for (int r = 0; r < 12; r++) emit<N, LSB>(out_blk, k, t + NB * r, u[r]);
+    }
+}
+
 __device__ __forceinline__ void load_frame(const int *__restrict__ in32, int blk, int k, int (&x)[16])
 {
+    if constexpr (SDDC_BUF) {
+        const __amdgpu_buffer_rsrc_t rs = buf_rsrc(in32 + ((size_t)blk * BLOCK + (size_t)k * HOP) / 2);
+        const unsigned vo = 4u * threadIdx.x;
+#pragma unroll
+        for (int r = 0; r < 16; r++) x[r] = buf_load4(rs, vo, 4u * NT * r);
+        return;
+    }
     const int *p = in32 + ((size_t)blk * BLOCK + (size_t)k * HOP) / 2 + threadIdx.x;
 #pragma unroll
     for (int r = 0; r < 16; r++) x[r] = p[NT * r];
@@ -152,8 +231,7 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
     const float2 *__restrict__ rec_f, const float2 *__restrict__ rec_i,
     const float2 *__restrict__ twt_f, const float2 *__restrict__ twt_i,
     const float2 *__restrict__ post8192, const float2 *__restrict__ hsel,
-    const float *__restrict__ rsel, const float2 *__restrict__ uph,
-    int tunebin, unsigned zmask)
+    const float4 *__restrict__ pq, int tunebin)
 {
     constexpr int N = HALF >> D;
     __shared__ __attribute__((aligned(16))) float2 lds[kDB ? 2 * HALF : HALF];
@@ -178,19 +256,6 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
         }
     }
     const float2 pb_ = post8192[(tunebin + tid) & 8191];   // W_8192^{tb + tid}
-    // Filter kept in registers (N >= 512): H_d[k] = W_4096^{3583 k} R_d[k] with R_d real, because
-    // the 1025 time-reversed taps at ht[3071..4095] are symmetric about 3583 (fft_mt_r2iq.cpp:200-203).
-    // Thread t needs k = t + 256 r (+ 4096 - N when wrapped): R_d per r, phase W^{3583 t} x constants.
-    constexpr int R0H = N >= 512 ? N / 256 : 1;
-    float hr[R0H];
-    float2 u_ = make_float2(1.f, 0.f), v_ = make_float2(1.f, 0.f);
-    if constexpr (SDDC_HREG && N >= 512) {
-#pragma unroll
-        for (int r = 0; r < R0H; r++) hr[r] = rsel[tid + NT * r];
-        u_ = uph[tid];                 // W_4096^{3583 t}
-        v_ = cmul(pb_, u_);
-    }
-
     for (int i = tid; i < 15 * 16 + 15 * SQ; i += NT)
         twl[i] = i < 15 * 16 ? tw_p1[i] : tw_q1[i - 15 * 16];   // visible after the first frame's pass-0 barrier
 
@@ -206,9 +271,10 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
         asm volatile("" : "+s"(z));
         const int t = tid + z;
         const float2 *hs = hsel + z, *pst = post8192 + z;
+        const float4 *pqz = pq + z;
         const float2 *ttf = twt_f + z, *tti = twt_i + z;
-        float2 fw1 = fw1_, fw4 = fw4_, iw1 = iw1_, iw4 = iw4_, pb = pb_, uu = u_, vv = v_;
-        asm volatile("" : "+v"(fw1), "+v"(fw4), "+v"(iw1), "+v"(iw4), "+v"(pb), "+v"(uu), "+v"(vv));
+        float2 fw1 = fw1_, fw4 = fw4_, iw1 = iw1_, iw4 = iw4_, pb = pb_;
+        asm volatile("" : "+v"(fw1), "+v"(fw4), "+v"(iw1), "+v"(iw4), "+v"(pb));
         const int sT = swz(t);            // swz(t + 256 r) = sT + 256 r
         const int x15 = t & 15;
         float2 *out_blk = out + (size_t)blk * 8 * N;
@@ -275,6 +341,9 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
                 const int b0 = tunebin + t;                  // bin of r = 0
                 const int sb0 = swz(b0);                     // swz(b0 + 256 r - N w) = sb0 + 256 r - N w
                 const int sc0 = swz(HALF - b0);              // mirror bin, same separability
+                const char *w0b = reinterpret_cast<const char *>(w0);
+                const unsigned sb0b = 8u * (unsigned)sb0, sc0b = 8u * (unsigned)sc0, tb16 = 16u * (unsigned)t;
+                const __amdgpu_buffer_rsrc_t rpq = buf_rsrc(pqz);
                 float2 a[R0];
 #pragma unroll
                 for (int r = 0; r < R0; r++) {
@@ -282,33 +351,34 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
                     const int sh = NT * r - (wrap ? N : 0);
                     const int bin = b0 + sh;
                     const int q = (r - (wrap ? N / NT : 0)) & 31;       // W_8192^{256 r - N wrap}
-                    // branch-free: read a clamped (valid) address, zero the result if out of range
-                    if (SDDC_ZSKIP && ((zmask >> r) & 1)) {   // wave-uniform: whole range zero-filled
-                        a[r] = make_float2(0.f, 0.f);
+                    // branch-free: read a valid (wrapped) address; out-of-band bins have P = Q = 0
+                    if constexpr (SDDC_PQ) {
+                        // byte offsets: the wrap is one AND, the scale folds away
+                        const float2 zk = *reinterpret_cast<const float2 *>(
+                            w0b + ((sb0b + 8u * (unsigned)sh) & (8u * HALF - 8u)));
+                        const float2 zc = *reinterpret_cast<const float2 *>(
+                            w0b + ((sc0b - 8u * (unsigned)sh) & (8u * HALF - 8u)));
+                        float4 c;
+                        if constexpr (SDDC_FAKE & 1)
+                            c = make_float4(0.5f, 0.25f * r, 0.1f, 0.2f);
+                        else if constexpr (SDDC_BUF)
+                            c = buf_load16(rpq, tb16, 16u * NT * r);
+                        else
+                            c = *reinterpret_cast<const float4 *>(reinterpret_cast<const char *>(pqz + NT * r) + tb16);
+                        a[r] = split_pq(zk, zc, c);
                         continue;
                     }
-                    const bool ok = (unsigned)bin < (unsigned)HALF;
                     const float2 zk = w0[(sb0 + sh) & (HALF - 1)];
                     const float2 zc = w0[(sc0 - sh) & (HALF - 1)];
-                    const float2 A = make_float2(zk.x + zc.x, zk.y - zc.y);
-                    const float2 Bi = make_float2(zk.y + zc.y, zc.x - zk.x);   // (Zk - conj Zc)/i
-                    float2 val;
-                    if constexpr (SDDC_HREG) {
-                        // T = R/2 [A W^{3583k} + Bi W_8192^{bin} W^{3583k}]; both phases are a
-                        // per-thread base (uu, vv) times a compile-time W_32 power
-                        const int eE = (3840 * r + (wrap ? 3583 * (HALF - N) : 0)) & (HALF - 1);
-                        const int qE = (eE / 128) & 31;
-                        const int qF = ((NT * r - (wrap ? N : 0)) / 256 + 2 * eE / 256) & 31;
-                        const float2 ue = cmul(uu, make_float2(kW32re[qE], kW32im[qE]));
-                        const float2 vf = cmul(vv, make_float2(kW32re[qF], kW32im[qF]));
-                        const float2 y = cadd(cmul(A, ue), cmul(Bi, vf));
-                        val = make_float2(y.x * hr[r], y.y * hr[r]);
-                    } else {
+                    {
+                        const bool ok = (unsigned)bin < (unsigned)HALF;
+                        const float2 A = make_float2(zk.x + zc.x, zk.y - zc.y);
+                        const float2 Bi = make_float2(zk.y + zc.y, zc.x - zk.x);   // (Zk - conj Zc)/i
                         const float2 wb = cmul(pb, make_float2(kW32re[q], kW32im[q]));
                         const float2 hv = (SDDC_FAKE & 1) ? make_float2(0.5f, 0.25f * r) : hs[t + NT * r];
-                        val = cmul(cadd(A, cmul(Bi, wb)), hv);
+                        const float2 val = cmul(cadd(A, cmul(Bi, wb)), hv);
+                        a[r] = ok ? val : make_float2(0.f, 0.f);
                     }
-                    a[r] = ok ? val : make_float2(0.f, 0.f);
                 }
                 dft<R0, +1>(a, u);
             }
@@ -368,13 +438,7 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
                     twiddle_rec16<+1>(a, iw1, iw4);
                 }
                 dft16<+1>(a, u);
-                if (kc == 0) {
-#pragma unroll
-                    for (int r = 4; r < 12; r++) emit<N, LSB>(out_blk, 0, t + NB * r, u[r]);
-                } else {
-#pragma unroll
-                    for (int r = 0; r < 12; r++) emit<N, LSB>(out_blk, kc, t + NB * r, u[r]);
-                }
+                emit_frame<N, NB, LSB>(out_blk, kc, t, u);
             }
         } else {
             // ---- N <= 256: materialise the N filtered bins, then [N/16, 16] ----
@@ -383,7 +447,10 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
             if (t < N) {
                 const int m = t;
                 const int bin = tunebin + m - (m >= N / 2 ? N : 0);
-                tv = split_bin(w0, bin, pst[bin & 8191], hs[m]);
+                if constexpr (SDDC_PQ)
+                    tv = split_pq(w0[swz(bin & (HALF - 1))], w0[swz((HALF - bin) & (HALF - 1))], pqz[m]);
+                else
+                    tv = split_bin(w0, bin, pst[bin & 8191], hs[m]);
             }
             if constexpr (!kDB) LOOP_SYNC();
             if (t < N) w1[swz(t)] = tv;
@@ -409,13 +476,7 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
 #pragma unroll
                 for (int r = 1; r < 16; r++) a[r] = cmulc(a[r], twl[15 * 16 + (r - 1) * NB + t]);
                 dft16<+1>(a, u);
-                if (kc == 0) {
-#pragma unroll
-                    for (int r = 4; r < 12; r++) emit<N, LSB>(out_blk, 0, t + NB * r, u[r]);
-                } else {
-#pragma unroll
-                    for (int r = 0; r < 12; r++) emit<N, LSB>(out_blk, kc, t + NB * r, u[r]);
-                }
+                emit_frame<N, NB, LSB>(out_blk, kc, t, u);
             }
         }
         if constexpr (kDB) {   // the next frame writes the buffer this frame's last pass did not read
@@ -426,25 +487,35 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
     }
 }
 
-// Bit r set: for inverse pass-0 leg r every thread's bin tb + t + 256 r (- N if wrapped) lies
-// outside [0, 4096), i.e. the reference zero-fills the whole leg (impl.hpp:91-92, 95-96).
-unsigned zero_bins_mask(int N, int tunebin)
+// Split x filter coefficients for one (d, tunebin): pq[m] = (P, Q) of inverse input m, with
+// bin = tb + m - (m >= N/2 ? N : 0) (fft_mt_r2iq_impl.hpp:84-98); zero outside [0, 4096).
+// Evaluated in double from the float tables and rounded once.
+__global__ void build_split_filter_kernel(const float2 *__restrict__ hsel, const float2 *__restrict__ post8192,
+                                          int N, int tunebin, float4 *__restrict__ pq)
 {
-    unsigned m = 0;
-    if (N < 512) return 0;
-    for (int r = 0; r < N / 256; r++) {
-        const int lo = tunebin + NT * r - (NT * r >= N / 2 ? N : 0);
-        if (lo + NT - 1 < 0 || lo >= HALF) m |= 1u << r;
+    const int m = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (m >= N) return;
+    const int bin = tunebin + m - (m >= N / 2 ? N : 0);
+    float4 c = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (bin >= 0 && bin < HALF) {
+        const double hr = hsel[m].x, hi = hsel[m].y;
+        const double wr = post8192[bin].x, wi = post8192[bin].y;
+        // 1 - i W = (1 + wi, -wr), 1 + i W = (1 - wi, wr)
+        const double pr = 1.0 + wi, pi = -wr, qr = 1.0 - wi, qi = wr;
+        c.x = (float)(hr * pr - hi * pi);
+        c.y = (float)(hr * pi + hi * pr);
+        c.z = (float)(hr * qr - hi * qi);
+        c.w = (float)(hr * qi + hi * qr);
     }
-    return m;
+    pq[m] = c;
 }
 
 int g_occupancy[7][4] = {};
 int g_cus = 0;
 
 template <int D, bool RAND, bool LSB>
-hipError_t launch_v(const KernelTables &t, const int16_t *d_in, int nblk, float *d_out, int tunebin,
-                    int device, hipStream_t s)
+hipError_t launch_v(const KernelTables &t, const int16_t *d_in, int nblk, float *d_out, const float4 *pq,
+                    int tunebin, int device, hipStream_t s)
 {
     auto kern = r2iq_persistent_kernel<D, RAND, LSB>;
     int &occ = g_occupancy[D][(RAND ? 2 : 0) + (LSB ? 1 : 0)];
@@ -463,35 +534,43 @@ hipError_t launch_v(const KernelTables &t, const int16_t *d_in, int nblk, float 
     if (grid > nframes) grid = nframes;
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), 0, s, reinterpret_cast<const int *>(d_in),
                        reinterpret_cast<float2 *>(d_out), nframes, t.tw_p1, t.tw_q1[D], t.rec_f, t.rec_i[D],
-                       t.twt_f, t.twt_i[D], t.post8192, t.hsel[D], t.rsel[D], t.uph, tunebin,
-                       zero_bins_mask(HALF >> D, tunebin));
+                       t.twt_f, t.twt_i[D], t.post8192, t.hsel[D], pq, tunebin);
     return hipGetLastError();
 }
 
 template <int D>
-hipError_t launch_d(const KernelTables &t, const int16_t *d_in, int nblk, float *d_out, int tunebin,
-                    int lsb, int rand, int device, hipStream_t s)
+hipError_t launch_d(const KernelTables &t, const int16_t *d_in, int nblk, float *d_out, const float4 *pq,
+                    int tunebin, int lsb, int rand, int device, hipStream_t s)
 {
     if (rand)
-        return lsb ? launch_v<D, true, true>(t, d_in, nblk, d_out, tunebin, device, s)
-                   : launch_v<D, true, false>(t, d_in, nblk, d_out, tunebin, device, s);
-    return lsb ? launch_v<D, false, true>(t, d_in, nblk, d_out, tunebin, device, s)
-               : launch_v<D, false, false>(t, d_in, nblk, d_out, tunebin, device, s);
+        return lsb ? launch_v<D, true, true>(t, d_in, nblk, d_out, pq, tunebin, device, s)
+                   : launch_v<D, true, false>(t, d_in, nblk, d_out, pq, tunebin, device, s);
+    return lsb ? launch_v<D, false, true>(t, d_in, nblk, d_out, pq, tunebin, device, s)
+               : launch_v<D, false, false>(t, d_in, nblk, d_out, pq, tunebin, device, s);
 }
 
 }  // namespace
 
+hipError_t launch_build_split_filter(const KernelTables &t, int d, int tunebin, float4 *pq, hipStream_t s)
+{
+    if (d < 0 || d > 6) return hipErrorInvalidValue;
+    const int N = HALF >> d;
+    hipLaunchKernelGGL(build_split_filter_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, t.hsel[d],
+                       t.post8192, N, tunebin, pq);
+    return hipGetLastError();
+}
+
 hipError_t launch_frames_persistent(const KernelTables &t, int d, const int16_t *d_in, int nblk, float *d_out,
-                                    int tunebin, int lsb, int rand, int device, hipStream_t s)
+                                    const float4 *pq, int tunebin, int lsb, int rand, int device, hipStream_t s)
 {
     switch (d) {
-    case 0: return launch_d<0>(t, d_in, nblk, d_out, tunebin, lsb, rand, device, s);
-    case 1: return launch_d<1>(t, d_in, nblk, d_out, tunebin, lsb, rand, device, s);
-    case 2: return launch_d<2>(t, d_in, nblk, d_out, tunebin, lsb, rand, device, s);
-    case 3: return launch_d<3>(t, d_in, nblk, d_out, tunebin, lsb, rand, device, s);
-    case 4: return launch_d<4>(t, d_in, nblk, d_out, tunebin, lsb, rand, device, s);
-    case 5: return launch_d<5>(t, d_in, nblk, d_out, tunebin, lsb, rand, device, s);
-    case 6: return launch_d<6>(t, d_in, nblk, d_out, tunebin, lsb, rand, device, s);
+    case 0: return launch_d<0>(t, d_in, nblk, d_out, pq, tunebin, lsb, rand, device, s);
+    case 1: return launch_d<1>(t, d_in, nblk, d_out, pq, tunebin, lsb, rand, device, s);
+    case 2: return launch_d<2>(t, d_in, nblk, d_out, pq, tunebin, lsb, rand, device, s);
+    case 3: return launch_d<3>(t, d_in, nblk, d_out, pq, tunebin, lsb, rand, device, s);
+    case 4: return launch_d<4>(t, d_in, nblk, d_out, pq, tunebin, lsb, rand, device, s);
+    case 5: return launch_d<5>(t, d_in, nblk, d_out, pq, tunebin, lsb, rand, device, s);
+    case 6: return launch_d<6>(t, d_in, nblk, d_out, pq, tunebin, lsb, rand, device, s);
     default: return hipErrorInvalidValue;
     }
 }

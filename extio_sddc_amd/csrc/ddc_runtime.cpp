@@ -85,6 +85,13 @@ struct sddc_ddc {
 
     int *d_tunebins = nullptr;             // channel tune bins (device)
     std::vector<int> tunebins_cached;
+
+    // split x filter coefficients of the current (d, tunebin), rebuilt on device when either
+    // changes; pq_used marks the last launch that read them (possibly on another stream)
+    float4 *d_pq = nullptr;
+    int pq_d = -1, pq_tb = -1;
+    hipEvent_t pq_used = nullptr;
+    hipStream_t pq_stream = nullptr;
 };
 
 extern "C" {
@@ -172,9 +179,6 @@ int sddc_ddc_create(float gain, int device, sddc_ddc_t **out)
     for (int r = 1; r < 16; r++)
         for (int j = 0; j < 256; j++) host[o_twtf + (r - 1) * 256 + j] = W((double)j * r, 4096);
     size_t o_hsel[SDDC_DDC_NDEC], o_q1[SDDC_DDC_NDEC], o_reci[SDDC_DDC_NDEC], o_twti[SDDC_DDC_NDEC];
-    size_t o_rsel[SDDC_DDC_NDEC];
-    const size_t o_uph = put(256);
-    for (int j = 0; j < 256; j++) host[o_uph + j] = W(3583.0 * j, 4096);
     std::vector<std::complex<double>> H(SDDC_DDC_HALF_FFT);
     for (int d = 0; d < SDDC_DDC_NDEC; d++) {
         const int mfft = SDDC_DDC_HALF_FFT >> d;
@@ -185,15 +189,6 @@ int sddc_ddc_create(float gain, int device, sddc_ddc_t **out)
             // (impl.hpp:90,94 with filter2 = filter + halfFft - mfft/2, impl.hpp:7)
             const std::complex<double> v = H[m < mfft / 2 ? m : SDDC_DDC_HALF_FFT - mfft + m];
             host[o_hsel[d] + m] = make_float2((float)(0.5 * v.real()), (float)(0.5 * v.imag()));
-        }
-        // real amplitude R_d[k] = H_d[k] W^{-3583 k} (the taps are symmetric, so H_d has linear
-        // phase); two floats per float2 slot
-        o_rsel[d] = put((mfft + 1) / 2);
-        for (int m = 0; m < mfft; m++) {
-            const int kk = m < mfft / 2 ? m : SDDC_DDC_HALF_FFT - mfft + m;
-            const double a = 2.0 * M_PI * 3583.0 * kk / 4096.0;
-            const double R = H[kk].real() * std::cos(a) - H[kk].imag() * std::sin(a);
-            reinterpret_cast<float *>(&host[o_rsel[d]])[m] = (float)(0.5 * R);
         }
         // inverse pass-1 table W_{16S}^{s r}, S = mfft/256 (mfft >= 512) or mfft/16
         const int S = mfft >= 512 ? mfft / 256 : mfft / 16;
@@ -216,6 +211,8 @@ int sddc_ddc_create(float gain, int device, sddc_ddc_t **out)
     hipError_t e = hipMalloc(&h->d_tables, ntab * sizeof(float2));
     if (e == hipSuccess) e = hipMemcpy(h->d_tables, host.data(), ntab * sizeof(float2), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipMalloc(&h->d_pq, SDDC_DDC_HALF_FFT * sizeof(float4));
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&h->pq_used, hipEventDisableTiming);
     if (e != hipSuccess) {
         sddc_ddc_destroy(h);
         return fail(SDDC_ERR_HIP, "create: %s", hipGetErrorString(e));
@@ -226,13 +223,11 @@ int sddc_ddc_create(float gain, int device, sddc_ddc_t **out)
     h->tables.tw_p1 = T + o_p1;
     h->tables.rec_f = T + o_recf;
     h->tables.twt_f = T + o_twtf;
-    h->tables.uph = T + o_uph;
     for (int d = 0; d < SDDC_DDC_NDEC; d++) {
         h->tables.hsel[d] = T + o_hsel[d];
         h->tables.tw_q1[d] = T + o_q1[d];
         h->tables.rec_i[d] = T + o_reci[d];
         h->tables.twt_i[d] = T + o_twti[d];
-        h->tables.rsel[d] = reinterpret_cast<const float *>(T + o_rsel[d]);
     }
     *out = h;
     return SDDC_OK;
@@ -248,6 +243,8 @@ int sddc_ddc_destroy(sddc_ddc_t *h)
         if (h->d_in) (void)hipFree(h->d_in);
         if (h->d_out) (void)hipFree(h->d_out);
         if (h->d_tunebins) (void)hipFree(h->d_tunebins);
+        if (h->d_pq) (void)hipFree(h->d_pq);
+        if (h->pq_used) (void)hipEventDestroy(h->pq_used);
         if (h->h_in) (void)hipHostFree(h->h_in);
         if (h->h_out) (void)hipHostFree(h->h_out);
         if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -316,8 +313,21 @@ static hipError_t launch_single(sddc_ddc_t *h, const int16_t *d_in, int nblk, fl
 {
     if (h->variant == 1)
         return sddc::launch_frames(h->tables, h->d, d_in, nblk, d_out, h->tunebin, h->lsb, h->rand, s);
-    return sddc::launch_frames_persistent(h->tables, h->d, d_in, nblk, d_out, h->tunebin, h->lsb, h->rand,
-                                          h->device, s);
+    if (h->pq_d != h->d || h->pq_tb != h->tunebin) {
+        if (h->pq_stream && h->pq_stream != s) {   // a launch on another stream may still read d_pq
+            hipError_t e = hipStreamWaitEvent(s, h->pq_used, 0);
+            if (e != hipSuccess) return e;
+        }
+        hipError_t e = sddc::launch_build_split_filter(h->tables, h->d, h->tunebin, h->d_pq, s);
+        if (e != hipSuccess) return e;
+        h->pq_d = h->d;
+        h->pq_tb = h->tunebin;
+    }
+    hipError_t e = sddc::launch_frames_persistent(h->tables, h->d, d_in, nblk, d_out, h->d_pq, h->tunebin,
+                                                  h->lsb, h->rand, h->device, s);
+    if (e != hipSuccess) return e;
+    h->pq_stream = s;
+    return hipEventRecord(h->pq_used, s);
 }
 
 /* internal (not in include/sddc_ddc.h): kernel variant for A/B timing, see sddc_ddc_internal.h */
@@ -342,6 +352,7 @@ int sddc_ddc_process_device(sddc_ddc_t *h, const int16_t *d_in, int nblk, float 
 {
     int rc = check_process_args(h, d_in, nblk, d_out);
     if (rc) return rc;
+    std::lock_guard<std::mutex> lk(h->mu);
     DeviceGuard g(h->device);
     HIP_TRY(g.err);
     HIP_TRY(launch_single(h, d_in, nblk, d_out, (hipStream_t)hip_stream));
