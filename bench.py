@@ -113,6 +113,8 @@ def main() -> None:
     ap.add_argument("--channels", type=int, default=1024)
     ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds of CPU-baseline work")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--fine-tune", type=float, default=0.0,
+                    help="fused fine-tune NCO frequency (fraction of the output rate); 0 = off")
     args = ap.parse_args()
 
     import torch
@@ -134,6 +136,11 @@ def main() -> None:
     ddc = R2iq(gain=1.0, device=local)
     ddc.setDecimate(d)
     ddc.setTuneBin(args.tunebin)
+    if args.fine_tune:
+        if args.mode != "single":
+            raise SystemExit("--fine-tune is single-channel only")
+        ddc.setFineTune(args.fine_tune)
+        args.no_cpu_baseline = True   # the CPU leg is the plain DDC
     stream = torch.cuda.current_stream()
 
     if args.mode == "single":
@@ -145,7 +152,7 @@ def main() -> None:
         def step():
             ddc.process_device(d_in, nblk, d_out, stream)
         samples_per_step_all = nblk * BLOCK * world
-        workload = f"single d={d} nblk={nblk}"
+        workload = f"single d={d} nblk={nblk}" + (f" fine_tune={args.fine_tune}" if args.fine_tune else "")
     else:
         from extio_sddc_amd.shard import broadcast_samples, channel_shard
         tbs_all = [4 * c for c in range(args.channels)]
@@ -200,7 +207,7 @@ def main() -> None:
         "scaling": "weak" if args.mode == "single" else "strong",
         "vs_baseline": None, "dtype": "f32 (int16 in, complex64 out)", "data": "synthetic",
         "config": {"workload": "single-channel DDC, 128 MS/s int16 in, decim=2, 1xMI355X"
-                   if (args.mode == "single" and d == 0) else workload,
+                   if (args.mode == "single" and d == 0 and not args.fine_tune) else workload,
                    "decim": 2 << d, "d": d, "tunebin": args.tunebin, "blocks_per_step_per_gpu": nblk,
                    "block_samples": BLOCK, "mode": args.mode,
                    "channels": args.channels if args.mode == "channels" else 1,

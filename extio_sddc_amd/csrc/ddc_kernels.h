@@ -30,9 +30,11 @@ hipError_t launch_frames(const KernelTables &t, int d, const int16_t *d_in, int 
 
 // v2 (default): persistent workgroups, input prefetch, swizzled LDS.  pq: the split x filter
 // coefficients of (d, tunebin), HALF >> d float4, built by launch_build_split_filter.
+// nco_starts/nco_trig: fused fine-tune NCO tables (fine_tune.h), or nullptr for none.
 hipError_t launch_frames_persistent(const KernelTables &t, int d, const int16_t *d_in, int nblk,
                                     float *d_out, const float4 *pq, int tunebin, int lsb, int rand,
-                                    int device, hipStream_t s);
+                                    const float2 *nco_starts, const float2 *nco_trig, int device,
+                                    hipStream_t s);
 hipError_t launch_build_split_filter(const KernelTables &t, int d, int tunebin, float4 *pq, hipStream_t s);
 
 int channels_per_group(int d, int nch);

@@ -184,9 +184,29 @@ __device__ __forceinline__ void emit(float2 *__restrict__ out_blk, int k, int n,
         out_blk[N / 2 + (3 * N / 4) * (k - 1) + n] = v;
 }
 
-// The kept outputs n = t + NB r of frame k (r in [4, 12) for k = 0, [0, 12) otherwise)
-template <int N, int NB, bool LSB>
-__device__ __forceinline__ void emit_frame(float2 *__restrict__ out_blk, int k, int t, const float2 (&u)[16])
+// Fine-tune NCO on output sample o of the batch (fine_tune.h): phasor T[q-1] * S_b[l] for
+// o = 128 b + 4 q + l, then the mix, in pf_mixer.cpp:808-833's float operation order.
+struct NcoArgs {
+    const float2 *starts;   // [blocks][4] lane starts of this batch (host chain)
+    const float2 *trig;     // [32] T
+};
+
+__device__ __forceinline__ float2 nco_mix(float2 v, const NcoArgs &nco, int o)
+{
+#pragma clang fp contract(off)
+    const float2 sb = nco.starts[(o >> 7) * 4 + (o & 3)];
+    const int q = (o >> 2) & 31;
+    const float2 tq = nco.trig[(q + 31) & 31];   // T[q-1]; unused for q = 0
+    const float2 pq = make_float2(tq.x * sb.x - tq.y * sb.y, tq.y * sb.x + tq.x * sb.y);
+    const float2 p = q ? pq : sb;
+    return make_float2(v.x * p.x - v.y * p.y, v.y * p.x + v.x * p.y);
+}
+
+// The kept outputs n = t + NB r of frame k (r in [4, 12) for k = 0, [0, 12) otherwise).
+// obase: the frame's first output slot relative to the batch (for the NCO).
+template <int N, int NB, bool LSB, bool NCO>
+__device__ __forceinline__ void emit_frame(float2 *__restrict__ out_blk, int k, int t, const float2 (&u)[16],
+                                           const NcoArgs &nco, int obase)
 {
     if constexpr (SDDC_BUF) {
         const __amdgpu_buffer_rsrc_t ro = buf_rsrc(out_blk + emit_base<N>(k));
@@ -197,10 +217,12 @@ __device__ __forceinline__ void emit_frame(float2 *__restrict__ out_blk, int k, 
             if (r < r0) continue;
             float2 v = u[r];
             if constexpr (LSB) v.y = -v.y;   // copy<flip=true>, fft_mt_r2iq.h:63-71
+            if constexpr (NCO) v = nco_mix(v, nco, obase + t + NB * r);
             buf_store8(v, ro, vo, 8u * NB * r);
         }
         return;
     }
+    static_assert(SDDC_BUF || !NCO, "the fused NCO needs the buffer-store output stage");
     if (k == 0) {
 #pragma unroll
         for (int r = 4; r < 12; r++) emit<N, LSB>(out_blk, 0, t + NB * r, u[r]);
@@ -224,14 +246,14 @@ __device__ __forceinline__ void load_frame(const int *__restrict__ in32, int blk
     for (int r = 0; r < 16; r++) x[r] = p[NT * r];
 }
 
-template <int D, bool RAND, bool LSB>
+template <int D, bool RAND, bool LSB, bool NCO>
 __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
     const int *__restrict__ in32, float2 *__restrict__ out, int nframes,
     const float2 *__restrict__ tw_p1, const float2 *__restrict__ tw_q1,
     const float2 *__restrict__ rec_f, const float2 *__restrict__ rec_i,
     const float2 *__restrict__ twt_f, const float2 *__restrict__ twt_i,
     const float2 *__restrict__ post8192, const float2 *__restrict__ hsel,
-    const float4 *__restrict__ pq, int tunebin)
+    const float4 *__restrict__ pq, int tunebin, NcoArgs nco)
 {
     constexpr int N = HALF >> D;
     __shared__ __attribute__((aligned(16))) float2 lds[kDB ? 2 * HALF : HALF];
@@ -278,6 +300,7 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
         const int sT = swz(t);            // swz(t + 256 r) = sT + 256 r
         const int x15 = t & 15;
         float2 *out_blk = out + (size_t)blk * 8 * N;
+        const int oblk = blk * 8 * N;   // NCO sample index of the block (batch-relative)
         const int kc = k;
         // ---- forward pass 0 (R16, NS1): convert + DFT16 from registers ----
         float2 v[16];
@@ -438,7 +461,7 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
                     twiddle_rec16<+1>(a, iw1, iw4);
                 }
                 dft16<+1>(a, u);
-                emit_frame<N, NB, LSB>(out_blk, kc, t, u);
+                emit_frame<N, NB, LSB, NCO>(out_blk, kc, t, u, nco, oblk + emit_base<N>(kc));
             }
         } else {
             // ---- N <= 256: materialise the N filtered bins, then [N/16, 16] ----
@@ -476,7 +499,7 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
 #pragma unroll
                 for (int r = 1; r < 16; r++) a[r] = cmulc(a[r], twl[15 * 16 + (r - 1) * NB + t]);
                 dft16<+1>(a, u);
-                emit_frame<N, NB, LSB>(out_blk, kc, t, u);
+                emit_frame<N, NB, LSB, NCO>(out_blk, kc, t, u, nco, oblk + emit_base<N>(kc));
             }
         }
         if constexpr (kDB) {   // the next frame writes the buffer this frame's last pass did not read
@@ -510,43 +533,55 @@ __global__ void build_split_filter_kernel(const float2 *__restrict__ hsel, const
     pq[m] = c;
 }
 
-int g_occupancy[7][4] = {};
+int g_occupancy[7][8] = {};
 int g_cus = 0;
 
-template <int D, bool RAND, bool LSB>
-hipError_t launch_v(const KernelTables &t, const int16_t *d_in, int nblk, float *d_out, const float4 *pq,
-                    int tunebin, int device, hipStream_t s)
+struct Launch {
+    const int16_t *d_in;
+    int nblk;
+    float *d_out;
+    const float4 *pq;
+    int tunebin;
+    int device;
+    hipStream_t s;
+    NcoArgs nco;
+};
+
+template <int D, bool RAND, bool LSB, bool NCO>
+hipError_t launch_v(const KernelTables &t, const Launch &L)
 {
-    auto kern = r2iq_persistent_kernel<D, RAND, LSB>;
-    int &occ = g_occupancy[D][(RAND ? 2 : 0) + (LSB ? 1 : 0)];
+    auto kern = r2iq_persistent_kernel<D, RAND, LSB, NCO>;
+    int &occ = g_occupancy[D][(RAND ? 4 : 0) + (LSB ? 2 : 0) + (NCO ? 1 : 0)];
     if (occ == 0) {
         int nb = 0;
         hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, NT, 0);
         if (e != hipSuccess) return e;
         int cus = 0;
-        e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+        e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, L.device);
         if (e != hipSuccess) return e;
         g_cus = cus;
         occ = nb > 0 ? nb : 1;
     }
-    const int nframes = nblk * FRAMES;
+    const int nframes = L.nblk * FRAMES;
     int grid = g_cus * occ;
     if (grid > nframes) grid = nframes;
-    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), 0, s, reinterpret_cast<const int *>(d_in),
-                       reinterpret_cast<float2 *>(d_out), nframes, t.tw_p1, t.tw_q1[D], t.rec_f, t.rec_i[D],
-                       t.twt_f, t.twt_i[D], t.post8192, t.hsel[D], pq, tunebin);
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), 0, L.s, reinterpret_cast<const int *>(L.d_in),
+                       reinterpret_cast<float2 *>(L.d_out), nframes, t.tw_p1, t.tw_q1[D], t.rec_f, t.rec_i[D],
+                       t.twt_f, t.twt_i[D], t.post8192, t.hsel[D], L.pq, L.tunebin, L.nco);
     return hipGetLastError();
 }
 
-template <int D>
-hipError_t launch_d(const KernelTables &t, const int16_t *d_in, int nblk, float *d_out, const float4 *pq,
-                    int tunebin, int lsb, int rand, int device, hipStream_t s)
+template <int D, bool RAND, bool LSB>
+hipError_t launch_n(const KernelTables &t, const Launch &L)
 {
-    if (rand)
-        return lsb ? launch_v<D, true, true>(t, d_in, nblk, d_out, pq, tunebin, device, s)
-                   : launch_v<D, true, false>(t, d_in, nblk, d_out, pq, tunebin, device, s);
-    return lsb ? launch_v<D, false, true>(t, d_in, nblk, d_out, pq, tunebin, device, s)
-               : launch_v<D, false, false>(t, d_in, nblk, d_out, pq, tunebin, device, s);
+    return L.nco.starts ? launch_v<D, RAND, LSB, true>(t, L) : launch_v<D, RAND, LSB, false>(t, L);
+}
+
+template <int D>
+hipError_t launch_d(const KernelTables &t, const Launch &L, int lsb, int rand)
+{
+    if (rand) return lsb ? launch_n<D, true, true>(t, L) : launch_n<D, true, false>(t, L);
+    return lsb ? launch_n<D, false, true>(t, L) : launch_n<D, false, false>(t, L);
 }
 
 }  // namespace
@@ -561,16 +596,18 @@ hipError_t launch_build_split_filter(const KernelTables &t, int d, int tunebin, 
 }
 
 hipError_t launch_frames_persistent(const KernelTables &t, int d, const int16_t *d_in, int nblk, float *d_out,
-                                    const float4 *pq, int tunebin, int lsb, int rand, int device, hipStream_t s)
+                                    const float4 *pq, int tunebin, int lsb, int rand, const float2 *nco_starts,
+                                    const float2 *nco_trig, int device, hipStream_t s)
 {
+    const Launch L{d_in, nblk, d_out, pq, tunebin, device, s, NcoArgs{nco_starts, nco_trig}};
     switch (d) {
-    case 0: return launch_d<0>(t, d_in, nblk, d_out, pq, tunebin, lsb, rand, device, s);
-    case 1: return launch_d<1>(t, d_in, nblk, d_out, pq, tunebin, lsb, rand, device, s);
-    case 2: return launch_d<2>(t, d_in, nblk, d_out, pq, tunebin, lsb, rand, device, s);
-    case 3: return launch_d<3>(t, d_in, nblk, d_out, pq, tunebin, lsb, rand, device, s);
-    case 4: return launch_d<4>(t, d_in, nblk, d_out, pq, tunebin, lsb, rand, device, s);
-    case 5: return launch_d<5>(t, d_in, nblk, d_out, pq, tunebin, lsb, rand, device, s);
-    case 6: return launch_d<6>(t, d_in, nblk, d_out, pq, tunebin, lsb, rand, device, s);
+    case 0: return launch_d<0>(t, L, lsb, rand);
+    case 1: return launch_d<1>(t, L, lsb, rand);
+    case 2: return launch_d<2>(t, L, lsb, rand);
+    case 3: return launch_d<3>(t, L, lsb, rand);
+    case 4: return launch_d<4>(t, L, lsb, rand);
+    case 5: return launch_d<5>(t, L, lsb, rand);
+    case 6: return launch_d<6>(t, L, lsb, rand);
     default: return hipErrorInvalidValue;
     }
 }

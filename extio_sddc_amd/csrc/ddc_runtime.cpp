@@ -19,6 +19,7 @@
 
 #include "ddc_kernels.h"
 #include "filterbank.h"
+#include "fine_tune.h"
 #include "sddc_ddc.h"
 #include "sddc_ddc_internal.h"
 
@@ -92,6 +93,18 @@ struct sddc_ddc {
     int pq_d = -1, pq_tb = -1;
     hipEvent_t pq_used = nullptr;
     hipStream_t pq_stream = nullptr;
+
+    // fused fine-tune NCO: host chain + per-launch [T | lane starts] staged through a
+    // pinned 3-slot ring into d_nco (stream-ordered copy before each launch)
+    float nco_fc = 0.f;
+    sddc::FineTune nco;
+    static constexpr int kNcoSlots = 3;
+    float2 *h_nco[kNcoSlots] = {};
+    hipEvent_t nco_ev[kNcoSlots] = {};
+    size_t h_nco_cap = 0;                  // float2 per slot
+    int nco_slot = 0;
+    float2 *d_nco = nullptr;
+    size_t d_nco_cap = 0;
 };
 
 extern "C" {
@@ -245,6 +258,11 @@ int sddc_ddc_destroy(sddc_ddc_t *h)
         if (h->d_tunebins) (void)hipFree(h->d_tunebins);
         if (h->d_pq) (void)hipFree(h->d_pq);
         if (h->pq_used) (void)hipEventDestroy(h->pq_used);
+        for (int i = 0; i < sddc_ddc::kNcoSlots; i++) {
+            if (h->h_nco[i]) (void)hipHostFree(h->h_nco[i]);
+            if (h->nco_ev[i]) (void)hipEventDestroy(h->nco_ev[i]);
+        }
+        if (h->d_nco) (void)hipFree(h->d_nco);
         if (h->h_in) (void)hipHostFree(h->h_in);
         if (h->h_out) (void)hipHostFree(h->h_out);
         if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -309,10 +327,59 @@ int sddc_ddc_reset(sddc_ddc_t *h)
     return SDDC_OK;
 }
 
+// Stage [T | lane starts of this launch's 128-sample blocks] for the fused NCO.
+static hipError_t stage_nco(sddc_ddc_t *h, int nblk, hipStream_t s)
+{
+    using sddc::FineTune;
+    const long nb = (long)nblk * (SDDC_DDC_BLOCK / 2 >> h->d) / FineTune::kBlock;
+    const size_t n = FineTune::kTable + (size_t)nb * FineTune::kLanes;
+    hipError_t e;
+    if (n > h->h_nco_cap) {
+        for (int i = 0; i < sddc_ddc::kNcoSlots; i++) {
+            if (h->nco_ev[i] && (e = hipEventSynchronize(h->nco_ev[i])) != hipSuccess) return e;
+            if (h->h_nco[i]) (void)hipHostFree(h->h_nco[i]);
+            h->h_nco[i] = nullptr;
+        }
+        h->h_nco_cap = 0;
+        for (int i = 0; i < sddc_ddc::kNcoSlots; i++) {
+            if ((e = hipHostMalloc(&h->h_nco[i], n * sizeof(float2), hipHostMallocDefault)) != hipSuccess) return e;
+            if (!h->nco_ev[i] && (e = hipEventCreateWithFlags(&h->nco_ev[i], hipEventDisableTiming)) != hipSuccess)
+                return e;
+        }
+        h->h_nco_cap = n;
+    }
+    if (n > h->d_nco_cap) {   // the previous launches may still read the old buffer
+        if (h->pq_stream && (e = hipStreamSynchronize(h->pq_stream)) != hipSuccess) return e;
+        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+        if (h->d_nco) (void)hipFree(h->d_nco);
+        h->d_nco = nullptr;
+        h->d_nco_cap = 0;
+        if ((e = hipMalloc(&h->d_nco, n * sizeof(float2))) != hipSuccess) return e;
+        h->d_nco_cap = n;
+    } else if (h->pq_stream && h->pq_stream != s) {   // a launch on another stream may still read d_nco
+        if ((e = hipStreamWaitEvent(s, h->pq_used, 0)) != hipSuccess) return e;
+    }
+    const int slot = h->nco_slot;
+    h->nco_slot = (slot + 1) % sddc_ddc::kNcoSlots;
+    if ((e = hipEventSynchronize(h->nco_ev[slot])) != hipSuccess) return e;   // its last copy is done
+    float2 *buf = h->h_nco[slot];
+    std::memcpy(buf, h->nco.table(), FineTune::kTable * sizeof(float2));
+    h->nco.starts(nb, buf + FineTune::kTable);
+    if ((e = hipMemcpyAsync(h->d_nco, buf, n * sizeof(float2), hipMemcpyHostToDevice, s)) != hipSuccess) return e;
+    return hipEventRecord(h->nco_ev[slot], s);
+}
+
 static hipError_t launch_single(sddc_ddc_t *h, const int16_t *d_in, int nblk, float *d_out, hipStream_t s)
 {
-    if (h->variant == 1)
+    if (h->variant == 1) {
+        if (h->nco_fc != 0.f) return hipErrorNotSupported;   // the v1 reference variant has no NCO stage
         return sddc::launch_frames(h->tables, h->d, d_in, nblk, d_out, h->tunebin, h->lsb, h->rand, s);
+    }
+    const bool nco = h->nco_fc != 0.f;
+    if (nco) {
+        hipError_t e = stage_nco(h, nblk, s);
+        if (e != hipSuccess) return e;
+    }
     if (h->pq_d != h->d || h->pq_tb != h->tunebin) {
         if (h->pq_stream && h->pq_stream != s) {   // a launch on another stream may still read d_pq
             hipError_t e = hipStreamWaitEvent(s, h->pq_used, 0);
@@ -323,11 +390,24 @@ static hipError_t launch_single(sddc_ddc_t *h, const int16_t *d_in, int nblk, fl
         h->pq_d = h->d;
         h->pq_tb = h->tunebin;
     }
-    hipError_t e = sddc::launch_frames_persistent(h->tables, h->d, d_in, nblk, d_out, h->d_pq, h->tunebin,
-                                                  h->lsb, h->rand, h->device, s);
+    hipError_t e = sddc::launch_frames_persistent(
+        h->tables, h->d, d_in, nblk, d_out, h->d_pq, h->tunebin, h->lsb, h->rand,
+        nco ? h->d_nco + sddc::FineTune::kTable : nullptr, nco ? h->d_nco : nullptr, h->device, s);
     if (e != hipSuccess) return e;
     h->pq_stream = s;
     return hipEventRecord(h->pq_used, s);
+}
+
+int sddc_ddc_set_fine_tune(sddc_ddc_t *h, float relative_freq)
+{
+    if (!h) return fail(SDDC_ERR_ARG, "null handle");
+    if (!std::isfinite(relative_freq)) return fail(SDDC_ERR_ARG, "fine tune: non-finite frequency");
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (relative_freq != h->nco_fc) {   // RadioHandler.cpp:291-296: re-init only on change
+        h->nco_fc = relative_freq;
+        if (relative_freq != 0.f) h->nco.init(relative_freq, 0.0f);
+    }
+    return SDDC_OK;
 }
 
 /* internal (not in include/sddc_ddc.h): kernel variant for A/B timing, see sddc_ddc_internal.h */
@@ -369,6 +449,7 @@ int sddc_ddc_process_channels_device(sddc_ddc_t *h, const int16_t *d_in, int nbl
     for (int c = 0; c < nch; c++)
         if (tunebins[c] < 0 || tunebins[c] >= SDDC_DDC_HALF_FFT)
             return fail(SDDC_ERR_ARG, "channel %d tune bin %d outside [0,4096)", c, tunebins[c]);
+    if (h->nco_fc != 0.f) return fail(SDDC_ERR_STATE, "fine-tune NCO is single-channel; set it to 0 first");
     const size_t need = (size_t)nblk * (size_t)(SDDC_DDC_OUT_BLOCK >> h->d) * 2;
     if (nch > 1 && out_stride_floats < need)
         return fail(SDDC_ERR_ARG, "out_stride_floats %zu < %zu floats per channel", out_stride_floats, need);

@@ -123,6 +123,12 @@ class R2iq:
     def setFreqOffset(self, offset: float) -> float:
         return float(self._L.sddc_ddc_set_freq_offset(self._h, offset))
 
+    def setFineTune(self, fc: float) -> None:
+        """Fused fine-tune NCO (the mixer RadioHandler applies after the r2iq, pf_mixer.cpp:
+        750-856 via RadioHandler.cpp:33-37); fc = the residual from setFreqOffset, 0 = off.
+        A new fc restarts the phase at 0, the same fc keeps it (RadioHandler.cpp:291-296)."""
+        check(self._L.sddc_ddc_set_fine_tune(self._h, float(fc)))
+
     def setTuneBin(self, tunebin: int) -> None:
         check(self._L.sddc_ddc_set_tunebin(self._h, tunebin))
 

@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define SDDC_DDC_ABI_VERSION 1
+#define SDDC_DDC_ABI_VERSION 2   /* 2: + sddc_ddc_set_fine_tune */
 
 #define SDDC_DDC_HALF_FFT   4096    /* halfFft               fft_mt_r2iq.h:18 */
 #define SDDC_DDC_FFTN       8192    /* FFTN_R_ADC            config.h:49 */
@@ -91,14 +91,27 @@ int   sddc_ddc_get_tunebin(const sddc_ddc_t *h);
  * 0 <= offset < 1 (fraction of Fs/2); outside it the tune bin is clamped into
  * [0, 4092] (the reference would read out of range, impl.hpp:76-79). */
 float sddc_ddc_set_freq_offset(sddc_ddc_t *h, float offset);
-/* TurnOn() stream reset (fft_mt_r2iq.cpp:111-129): zero history, seq = 0. */
+/* TurnOn() stream reset (fft_mt_r2iq.cpp:111-129): zero history, seq = 0.  The
+ * fine-tune NCO keeps its phase (the reference's mixer state lives in RadioHandler). */
 int   sddc_ddc_reset(sddc_ddc_t *h);
+
+/* Fused fine-tune NCO: mixes the output with the reference's
+ * fine-tune mixer, pf_mixer's shift_limited_unroll_C_sse (Core/pffft/pf_mixer.cpp:
+ * 750-856), as RadioHandlerClass::OnDataPacket does after the r2iq when fc != 0
+ * (Core/RadioHandler.cpp:33-37).  relative_freq = fc, the residual returned by
+ * sddc_ddc_set_freq_offset; a new fc restarts the phase at 0 like
+ * shift_limited_unroll_C_sse_init(fc, 0) (RadioHandler.cpp:291-296), the same fc keeps
+ * it; 0 turns the mixer off.  While on, process_device / process_host advance the
+ * mixer phase by their output length (stream order), and the single-channel path
+ * only: process_channels_device returns SDDC_ERR_STATE.  Not for the drop-in class,
+ * whose caller (RadioHandler) still mixes on the CPU. */
+int   sddc_ddc_set_fine_tune(sddc_ddc_t *h, float relative_freq);
 
 /* Complex samples produced per nblk input blocks at decimation d: nblk*(32768>>d). */
 size_t sddc_ddc_output_samples(int d, int nblk);
 
 /* ---- the hot loop (fft_mt_r2iq_impl.hpp:15-152) ---------------------------- */
-/* Stateless, device-resident.  d_in: device int16 [4096 + nblk*65536] = the
+/* Device-resident; stateless apart from the fine-tune NCO phase.  d_in: device int16 [4096 + nblk*65536] = the
  * 4096-sample history followed by nblk blocks (2-byte aligned; 4-byte aligned
  * start required).  d_out: device float [nblk*(32768>>d)*2], (I,Q) pairs, in
  * stream order.  Uses the handle's d / sideband / rand / tunebin.  Enqueued on

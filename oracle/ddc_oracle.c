@@ -344,3 +344,91 @@ void oracle_forward_r2c_f64(const int16_t *frame, int rand, double *X)
     memcpy(X, x, sizeof(double) * 2 * (OR_HALF_FFT + 1));
     free(x); free(w);
 }
+
+/* ------------------------------------------------------------------------------------------
+ * Fine-tune NCO: restatement of ALGO H, the x86/SSE build of
+ * shift_limited_unroll_C_sse_init / _inp_c (Core/pffft/pf_mixer.cpp:750-856), applied by
+ * RadioHandlerClass::OnDataPacket to every 32768-sample output buffer when fc != 0
+ * (Core/RadioHandler.cpp:33-37), with init(fc, 0) on every fc change (:291-296).
+ * Four lanes (SIMD_SZ, pf_mixer.h:134) carry the phasors of samples 4j+lane; blocks of
+ * 128 samples (UNROLL_SIZE, pf_mixer.h:133) multiply the lane starts by a table of
+ * 4(j+1)-step phasors, and the starts are renormalised after every block.  Plain float
+ * arithmetic in the SSE operation order (mul, mul, sub/add; sqrt; div), no fused ops.
+ * ------------------------------------------------------------------------------------------ */
+#define OR_NCO_LANES 4
+#define OR_NCO_BLOCK 128
+#define OR_NCO_PI ((float)3.14159265358979323846)          /* pf_mixer.cpp:40 */
+
+typedef struct {
+    float trig_c[OR_NCO_BLOCK / OR_NCO_LANES + 1];   /* dinterl_trig cos of entry i/4 */
+    float trig_s[OR_NCO_BLOCK / OR_NCO_LANES + 1];   /* dinterl_trig sin */
+    float start_c[OR_NCO_LANES], start_s[OR_NCO_LANES];   /* phase_state_i/q */
+} oracle_nco_t;
+
+/* pf_mixer.cpp:750-789 */
+void oracle_nco_init(float relative_freq, float phase_start_rad, oracle_nco_t *d)
+{
+    const float inc = 2 * relative_freq * OR_NCO_PI;
+    float ph = 0.0f;
+    for (int e = 0; e <= OR_NCO_BLOCK / OR_NCO_LANES; e++) {
+        for (int k = 0; k < OR_NCO_LANES; k++) {
+            ph += inc;
+            while (ph > OR_NCO_PI) ph -= 2 * OR_NCO_PI;
+            while (ph < -OR_NCO_PI) ph += 2 * OR_NCO_PI;
+        }
+        d->trig_c[e] = cosf(ph);
+        d->trig_s[e] = sinf(ph);
+    }
+    ph = phase_start_rad;
+    for (int k = 0; k < OR_NCO_LANES; k++) {
+        d->start_c[k] = cosf(ph);
+        d->start_s[k] = sinf(ph);
+        ph += inc;
+        while (ph > OR_NCO_PI) ph -= 2 * OR_NCO_PI;
+        while (ph < -OR_NCO_PI) ph += 2 * OR_NCO_PI;
+    }
+}
+
+/* pf_mixer.cpp:791-856; iq = interleaved (I,Q) float, n_cplx a multiple of 4 */
+void oracle_nco_apply(float *iq, int n_cplx, oracle_nco_t *d)
+{
+    float sc[OR_NCO_LANES], ss[OR_NCO_LANES], vc[OR_NCO_LANES], vs[OR_NCO_LANES];
+    for (int k = 0; k < OR_NCO_LANES; k++) {
+        sc[k] = vc[k] = d->start_c[k];
+        ss[k] = vs[k] = d->start_s[k];
+    }
+    while (n_cplx) {
+        const int nb = n_cplx >= OR_NCO_BLOCK ? OR_NCO_BLOCK : n_cplx;
+        for (int j = 0; j < nb / OR_NCO_LANES; j++) {
+            for (int k = 0; k < OR_NCO_LANES; k++) {
+                float *p = iq + 2 * (OR_NCO_LANES * j + k);
+                const float re = p[0], im = p[1];
+                const float a = re * vc[k], b = im * vs[k];
+                const float c = im * vc[k], e = re * vs[k];
+                p[0] = a - b;
+                p[1] = c + e;
+            }
+            for (int k = 0; k < OR_NCO_LANES; k++) {
+                const float tr = d->trig_c[j], ti = d->trig_s[j];
+                const float a = tr * sc[k], b = ti * ss[k];
+                const float c = ti * sc[k], e = tr * ss[k];
+                vc[k] = a - b;
+                vs[k] = c + e;
+            }
+        }
+        iq += 2 * nb;
+        n_cplx -= nb;
+        for (int k = 0; k < OR_NCO_LANES; k++) {
+            const float m2 = vc[k] * vc[k] + vs[k] * vs[k];
+            const float m = sqrtf(m2);
+            sc[k] = vc[k] = vc[k] / m;
+            ss[k] = vs[k] = vs[k] / m;
+        }
+    }
+    for (int k = 0; k < OR_NCO_LANES; k++) {
+        d->start_c[k] = sc[k];
+        d->start_s[k] = ss[k];
+    }
+}
+
+int oracle_nco_state_size(void) { return (int)sizeof(oracle_nco_t); }

@@ -17,6 +17,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libddc_oracle.so")
 REF_FIR_PATH = os.path.join(HERE, "_ref", "libref_fir.so")
+REF_MIXER_PATH = os.path.join(HERE, "_ref", "libref_mixer.so")
 
 HALF_FFT = 4096      # fft_mt_r2iq.h:18
 BLOCK = 65536        # config.h:80-81 transferSamples
@@ -52,6 +53,9 @@ def lib() -> ctypes.CDLL:
             fn.argtypes = [P, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, ctypes.c_int, P]
             fn.restype = ctypes.c_int
         L.oracle_forward_r2c_f64.argtypes = [P, ctypes.c_int, P]
+        L.oracle_nco_init.argtypes = [ctypes.c_float, ctypes.c_float, P]
+        L.oracle_nco_apply.argtypes = [P, ctypes.c_int, P]
+        L.oracle_nco_state_size.restype = ctypes.c_int
         L.oracle_init()
         _lib = L
     return _lib
@@ -150,6 +154,51 @@ def ref_kaiser(ntaps: int, astop: float, fpass: float, fstop: float) -> np.ndarr
     out = np.zeros(ntaps, np.float32)
     n = fn(ntaps, astop, fpass, fstop, out.ctypes.data)
     return out[:n]
+
+
+class Nco:
+    """Fine-tune NCO restatement (pf_mixer.cpp:750-856, ALGO H); stateful across apply()."""
+
+    def __init__(self, relative_freq: float, phase_start: float = 0.0):
+        L = lib()
+        self._st = ctypes.create_string_buffer(L.oracle_nco_state_size())
+        L.oracle_nco_init(relative_freq, phase_start, self._st)
+
+    def apply(self, iq: np.ndarray) -> np.ndarray:
+        """iq: complex64 (n multiple of 4); returns the mixed copy."""
+        buf = np.ascontiguousarray(iq, dtype=np.complex64).copy()
+        assert buf.size % 4 == 0
+        lib().oracle_nco_apply(buf.ctypes.data, buf.size, self._st)
+        return buf
+
+
+def ref_mixer_available() -> bool:
+    return os.path.exists(REF_MIXER_PATH)
+
+
+class RefMixer:
+    """The reference's own shift_limited_unroll_C_sse_{init,inp_c} (pf_mixer.cpp:750-856),
+    compiled into oracle/_ref by `make -C oracle ref` (build container only)."""
+
+    # shift_limited_unroll_C_sse_data_t (pf_mixer.h:204-216): 264 + 4 + 4 + 3 floats
+    class _State(ctypes.Structure):
+        _fields_ = [("dinterl_trig", ctypes.c_float * 264), ("phase_state_i", ctypes.c_float * 4),
+                    ("phase_state_q", ctypes.c_float * 4), ("dcos_blk", ctypes.c_float),
+                    ("dsin_blk", ctypes.c_float), ("phase_increment", ctypes.c_float)]
+
+    def __init__(self, relative_freq: float, phase_start: float = 0.0):
+        L = ctypes.CDLL(REF_MIXER_PATH)
+        L.shift_limited_unroll_C_sse_init.argtypes = [ctypes.c_float, ctypes.c_float]
+        L.shift_limited_unroll_C_sse_init.restype = RefMixer._State
+        L.shift_limited_unroll_C_sse_inp_c.argtypes = [ctypes.c_void_p, ctypes.c_int,
+                                                       ctypes.POINTER(RefMixer._State)]
+        self._L = L
+        self._st = L.shift_limited_unroll_C_sse_init(relative_freq, phase_start)
+
+    def apply(self, iq: np.ndarray) -> np.ndarray:
+        buf = np.ascontiguousarray(iq, dtype=np.complex64).copy()
+        self._L.shift_limited_unroll_C_sse_inp_c(buf.ctypes.data, buf.size, ctypes.byref(self._st))
+        return buf
 
 
 def max_rel_err(y: np.ndarray, ref: np.ndarray) -> float:

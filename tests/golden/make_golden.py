@@ -15,6 +15,13 @@ iq_golden.json
     r2iq is unbuildable here) so the GPU box can check the HIP
     path against fixed vectors as well as against the live oracle.
 
+nco_golden.json
+    Outputs of the REFERENCE's own fine-tune mixer, pf_mixer's ALGO H
+    (shift_limited_unroll_C_sse_{init,inp_c}, Core/pffft/pf_mixer.cpp:750-856),
+    compiled unmodified into oracle/_ref/libref_mixer.so by `make -C oracle ref`:
+    float32 bit patterns for seeded inputs fed in chunks (the state carries over),
+    and long-run probes of a unit input over 64 buffers of 32768 (phase drift).
+
     python tests/golden/make_golden.py
 """
 from __future__ import annotations
@@ -99,9 +106,64 @@ def iq_fixture() -> dict:
     return out
 
 
+NCO_CASES = [
+    # (fc, seed, chunk sizes in complex samples; multiples of 128 like the 32768 buffers)
+    (0.0123, 11, [512, 384]),
+    (-0.271, 12, [256, 128, 512]),
+    (0.4999, 13, [640]),
+    (1.0e-4, 14, [384, 256]),
+]
+NCO_LONG = [0.0123, -0.271]
+NCO_LONG_BUFFERS = 64
+NCO_BUFFER = 32768
+
+
+def nco_input(seed: int, n: int) -> np.ndarray:
+    rng = np.random.default_rng(seed)
+    return (rng.standard_normal(n) + 1j * rng.standard_normal(n)).astype(np.complex64) * np.float32(1000.0)
+
+
+def nco_probe_index() -> np.ndarray:
+    return np.arange(NCO_LONG_BUFFERS) * NCO_BUFFER + (np.arange(NCO_LONG_BUFFERS) * 997) % NCO_BUFFER
+
+
+def nco_fixture() -> dict:
+    if not O.ref_mixer_available():
+        raise SystemExit("oracle/_ref/libref_mixer.so missing: run `make -C oracle ref` where /root/reference exists")
+    out = {"source": "reference Core/pffft/pf_mixer.cpp shift_limited_unroll_C_sse_{init,inp_c}, "
+                     "built by oracle/Makefile `ref`; phase_start 0", "cases": [], "long": []}
+    for fc, seed, chunks in NCO_CASES:
+        x = nco_input(seed, sum(chunks))
+        m = O.RefMixer(fc)
+        y, o = [], 0
+        for c in chunks:
+            y.append(m.apply(x[o:o + c]))
+            o += c
+        y = np.concatenate(y)
+        out["cases"].append({"fc": fc, "seed": seed, "chunks": chunks,
+                             "out_f32_hex": f32hex(y.view(np.float32))})
+    idx = nco_probe_index()
+    for fc in NCO_LONG:
+        m = O.RefMixer(fc)
+        ones = np.ones(NCO_BUFFER, np.complex64)
+        probes = []
+        for b in range(NCO_LONG_BUFFERS):
+            yb = m.apply(ones)
+            probes.append(yb[idx[b] - b * NCO_BUFFER])
+        out["long"].append({"fc": fc, "buffers": NCO_LONG_BUFFERS, "buffer": NCO_BUFFER,
+                            "probe_f32_hex": f32hex(np.array(probes, np.complex64).view(np.float32))})
+    return out
+
+
 if __name__ == "__main__":
+    if "--nco-only" in sys.argv:
+        with open(os.path.join(HERE, "nco_golden.json"), "w") as f:
+            json.dump(nco_fixture(), f, indent=0)
+        raise SystemExit(0)
     with open(os.path.join(HERE, "kaiser_taps.json"), "w") as f:
         json.dump(kaiser_fixture(), f, indent=0)
     with open(os.path.join(HERE, "iq_golden.json"), "w") as f:
         json.dump(iq_fixture(), f, indent=0)
+    with open(os.path.join(HERE, "nco_golden.json"), "w") as f:
+        json.dump(nco_fixture(), f, indent=0)
     print("wrote", os.listdir(HERE))

@@ -66,7 +66,7 @@ def test_filter_response_matches_oracle(ddc_lib, oracle):
 
 def test_output_samples_and_constants(ddc_lib):
     from extio_sddc_amd import output_samples
-    assert ddc_lib.sddc_ddc_abi_version() == 1
+    assert ddc_lib.sddc_ddc_abi_version() == 2
     for d in range(7):
         assert ddc_lib.sddc_ddc_output_samples(d, 3) == 3 * (32768 >> d) == output_samples(d, 3)
     assert ddc_lib.sddc_ddc_output_samples(7, 1) == 0

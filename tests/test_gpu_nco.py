@@ -1,0 +1,126 @@
+"""Fused fine-tune NCO on the GPU (pytest -m gpu), through the C ABI.
+
+The product mixes in the DDC kernel's output stage with phasors T[q-1]*S_b built by
+the host chain (extio_sddc_amd/csrc/fine_tune.cpp).  Bars:
+  * bit-exact vs the oracle mixer (pinned bit-exact to the reference's pf_mixer.cpp,
+    tests/test_nco_cpu.py) applied to the same GPU DDC output;
+  * <= 1e-5 max-rel vs the f64 oracle DDC followed by the oracle mixer;
+  * stream continuity across calls, RadioHandler's re-init rule, off = plain DDC.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from extio_sddc_amd.synth import make_stream
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-5
+
+
+@pytest.fixture(scope="module")
+def torch_dev():
+    import torch
+    assert torch.cuda.is_available(), "gpu tests need a GPU"
+    return torch
+
+
+def _run(torch, r, x, nblk, d):
+    from extio_sddc_amd import output_samples
+    d_in = torch.from_numpy(np.ascontiguousarray(x)).to("cuda")
+    d_out = torch.full((output_samples(d, nblk) * 2,), float("nan"), dtype=torch.float32, device="cuda")
+    r.process_device(d_in, nblk, d_out)
+    torch.cuda.synchronize()
+    return d_out.cpu().numpy().view(np.complex64)
+
+
+def _ddc(d, tb, lsb=False, rand=False):
+    from extio_sddc_amd import R2iq
+    r = R2iq(gain=1.0)
+    r.setDecimate(d)
+    r.setTuneBin(tb)
+    r.setSideband(lsb)
+    r.updateRand(rand)
+    return r
+
+
+@pytest.mark.parametrize("d,tb,lsb,fc", [(0, 1024, False, 0.0123), (1, 284, True, -0.271),
+                                          (4, 2048, False, 0.4999), (6, 1024, False, 1e-4)])
+def test_fused_nco_bit_exact_vs_oracle_mixer(torch_dev, oracle, d, tb, lsb, fc):
+    nblk = 4 << min(d, 3)
+    x = make_stream(nblk, "mix")
+    with _ddc(d, tb, lsb) as r:
+        plain = _run(torch_dev, r, x, nblk, d)
+        r.setFineTune(fc)
+        mixed = _run(torch_dev, r, x, nblk, d)
+    ref = oracle.Nco(fc).apply(plain)
+    np.testing.assert_array_equal(mixed.view(np.uint32), ref.view(np.uint32))
+
+
+def test_fused_nco_vs_f64_oracle_pipeline(torch_dev, oracle):
+    d, tb, fc, nblk = 0, 1024, 0.0123, 8
+    x = make_stream(nblk, "mix")
+    H = oracle.filter_bank(1.0)
+    with _ddc(d, tb) as r:
+        r.setFineTune(fc)
+        y = _run(torch_dev, r, x, nblk, d)
+    ref = oracle.Nco(fc).apply(oracle.r2iq(x, nblk, d, tb, H=H).astype(np.complex64))
+    assert oracle.max_rel_err(y, ref) <= TOL
+
+
+def test_nco_phase_continues_across_calls(torch_dev):
+    """Two launches of 8 blocks (with their halos) == one launch of 16, bit-exact."""
+    d, nblk, fc = 1, 16, -0.271
+    x = make_stream(nblk, "uniform")
+    with _ddc(d, 1024) as r:
+        r.setFineTune(fc)
+        one = _run(torch_dev, r, x, nblk, d)
+    with _ddc(d, 1024) as r:
+        r.setFineTune(fc)
+        a = _run(torch_dev, r, x[:4096 + 8 * 65536], 8, d)
+        b = _run(torch_dev, r, x[8 * 65536:], 8, d)
+    np.testing.assert_array_equal(one.view(np.uint32), np.concatenate([a, b]).view(np.uint32))
+
+
+def test_nco_reinit_rule_and_off(torch_dev):
+    """Same fc keeps the phase, a new fc restarts at phase 0 (RadioHandler.cpp:291-296);
+    fc = 0 is the plain DDC (RadioHandler.cpp:33)."""
+    d, nblk = 2, 4
+    x = make_stream(nblk, "mix")
+    with _ddc(d, 1024) as r:
+        plain = _run(torch_dev, r, x, nblk, d)
+        r.setFineTune(0.1)
+        first = _run(torch_dev, r, x, nblk, d)
+        r.setFineTune(0.1)                      # unchanged: continues
+        second = _run(torch_dev, r, x, nblk, d)
+        assert not np.array_equal(first, second)
+        r.setFineTune(0.2)
+        r.setFineTune(0.1)                      # changed: restarts at phase 0
+        again = _run(torch_dev, r, x, nblk, d)
+        np.testing.assert_array_equal(first.view(np.uint32), again.view(np.uint32))
+        r.setFineTune(0.0)
+        off = _run(torch_dev, r, x, nblk, d)
+        np.testing.assert_array_equal(plain.view(np.uint32), off.view(np.uint32))
+
+
+def test_nco_host_path(torch_dev, oracle):
+    """process() (pinned staging, 64-block chunks) applies the same mixer."""
+    d, nblk, fc = 0, 70, 0.0123                 # > one 64-block host chunk
+    x = make_stream(nblk, "mix")
+    with _ddc(d, 1024) as r:
+        plain = r.process(x[4096:])
+        r.TurnOn()
+        r.setFineTune(fc)
+        mixed = r.process(x[4096:])
+    np.testing.assert_array_equal(mixed.view(np.uint32), oracle.Nco(fc).apply(plain).view(np.uint32))
+
+
+def test_nco_rejected_for_channels(torch_dev):
+    from extio_sddc_amd import DDCError
+    torch = torch_dev
+    with _ddc(4, 1024) as r:
+        r.setFineTune(0.1)
+        d_in = torch.zeros(4096 + 65536, dtype=torch.int16, device="cuda")
+        d_out = torch.empty(2 * 2048 * 2, dtype=torch.float32, device="cuda")
+        with pytest.raises(DDCError):
+            r.process_channels_device(d_in, 1, [100, 200], d_out)

@@ -12,5 +12,6 @@ hipcc --offload-arch=gfx950 $F $EXTRA -c $C/ddc_persistent.hip -o $O/p.o
 hipcc --offload-arch=gfx950 $F $EXTRA -c $C/ddc_channels.hip -o $O/c.o
 hipcc $F -ffp-contract=off -c $C/ddc_runtime.cpp -o $O/r.o
 hipcc $F -ffp-contract=off -c $C/filterbank.cpp -o $O/f.o
-hipcc --offload-arch=gfx950 -shared $O/k.o $O/p.o $O/c.o $O/r.o $O/f.o -o $R/build/ab/$NAME.so
+hipcc $F -ffp-contract=off -c $C/fine_tune.cpp -o $O/n.o
+hipcc --offload-arch=gfx950 -shared $O/k.o $O/p.o $O/c.o $O/r.o $O/f.o $O/n.o -o $R/build/ab/$NAME.so
 echo built $R/build/ab/$NAME.so
