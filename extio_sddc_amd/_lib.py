@@ -41,6 +41,7 @@ SIGNATURES = {
     "sddc_ddc_set_freq_offset": (_F, [_P, _F]),
     "sddc_ddc_reset": (_I, [_P]),
     "sddc_ddc_set_fine_tune": (_I, [_P, _F]),
+    "sddc_ddc_set_output_format": (_I, [_P, _I, _F]),
     "sddc_ddc_output_samples": (_SZ, [_I, _I]),
     "sddc_ddc_process_device": (_I, [_P, _P, _I, _P, _P]),
     "sddc_ddc_process_channels_device": (_I, [_P, _P, _I, _P, _I, _P, _SZ, _P]),

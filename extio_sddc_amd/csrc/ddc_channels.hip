@@ -9,13 +9,14 @@
 //           (Core/fft_mt_r2iq_impl.hpp:76-96), DFT-16 in registers, -> per-channel LDS slice
 //   pass B  radix-(N/16) Stockham step with W_256 twiddles from LDS, overlap-discard
 //           write of the kept outputs to the channel's stream (impl.hpp:117-138)
-// Channel c's output stream starts at out + c * stride (float2 units).  Persistent grid:
+// Channel c's output stream starts at complex element c * stride of out (CF32 or CS16).  Persistent grid:
 // CUs x resident workgroups, contiguous item ranges.
 #include <hip/hip_runtime.h>
 
 #include "ddc_consts.h"
 #include "ddc_kernels.h"
 #include "fft_device.hpp"
+#include "ddc_device_io.hpp"
 
 namespace sddc {
 namespace {
@@ -71,11 +72,12 @@ __device__ __forceinline__ constexpr float2 wsplit(int r)
     else return make_float2(kWsplitRe64[r], kWsplitIm64[r]);
 }
 
-template <int D, bool RAND, bool LSB>
+template <int D, bool RAND, bool CS16>
 __global__ __launch_bounds__(NT, 2) void r2iq_channels_v2_kernel(
-    const int *__restrict__ in32, float2 *__restrict__ out, size_t stride, int nframes,
+    const int *__restrict__ in32, void *__restrict__ out, size_t stride, int nframes,
     const int *__restrict__ tunebins, int nch, const float2 *__restrict__ tw_p1,
-    const float2 *__restrict__ rec_f, const float2 *__restrict__ post8192, const float2 *__restrict__ hsel)
+    const float2 *__restrict__ rec_f, const float2 *__restrict__ post8192, const float2 *__restrict__ hsel,
+    OutArgs oa)
 {
     constexpr int N = HALF >> D;
     static_assert(N <= 256 && N >= 64, "channels v2 covers d = 4..6");
@@ -185,7 +187,13 @@ __global__ __launch_bounds__(NT, 2) void r2iq_channels_v2_kernel(
             __syncthreads();
             // pass B: radix-RB Stockham step (NS = 16), twiddles W_N^{j q} = W_256^{(256/N) j q}
             if (cok) {
-                float2 *ob = out + (size_t)c * stride + (size_t)blk * 8 * N;
+                char *ob = static_cast<char *>(out) + ((size_t)c * stride + (size_t)blk * 8 * N) * out_bytes<CS16>();
+                auto put = [&](int idx, float2 o) {
+                    if constexpr (CS16)
+                        reinterpret_cast<unsigned *>(ob)[idx] = cs16_pack(o, oa.scale);
+                    else
+                        reinterpret_cast<float2 *>(ob)[idx] = o;
+                };
 #pragma unroll
                 for (int b = 0; b < BPT; b++) {
                     const int j = l + TPC * b;          // butterfly 0..15
@@ -200,12 +208,11 @@ __global__ __launch_bounds__(NT, 2) void r2iq_channels_v2_kernel(
                     for (int q = 0; q < RB; q++) {
                         const int n = j + 16 * q;
                         if (16 * q >= 3 * N / 4) continue;
-                        float2 o = y[q];
-                        if constexpr (LSB) o.y = -o.y;
+                        const float2 o = flip(y[q], oa.lsbmask);
                         if (k == 0) {
-                            if (16 * q >= N / 4) ob[n - N / 4] = o;
+                            if (16 * q >= N / 4) put(n - N / 4, o);
                         } else {
-                            ob[N / 2 + (3 * N / 4) * (k - 1) + n] = o;
+                            put(N / 2 + (3 * N / 4) * (k - 1) + n, o);
                         }
                     }
                 }
@@ -218,12 +225,12 @@ __global__ __launch_bounds__(NT, 2) void r2iq_channels_v2_kernel(
 int g_occ[3][4] = {};
 int g_cus = 0;
 
-template <int D, bool RAND, bool LSB>
+template <int D, bool RAND, bool CS16>
 hipError_t launch_v(const KernelTables &t, const int16_t *d_in, int nblk, const int *d_tunebins, int nch,
-                    float *d_out, size_t stride_floats, int device, hipStream_t s)
+                    void *d_out, size_t stride, OutArgs oa, int device, hipStream_t s)
 {
-    auto kern = r2iq_channels_v2_kernel<D, RAND, LSB>;
-    int &occ = g_occ[D - 4][(RAND ? 2 : 0) + (LSB ? 1 : 0)];
+    auto kern = r2iq_channels_v2_kernel<D, RAND, CS16>;
+    int &occ = g_occ[D - 4][(RAND ? 2 : 0) + (CS16 ? 1 : 0)];
     if (occ == 0) {
         int nb = 0;
         hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, NT, 0);
@@ -235,33 +242,33 @@ hipError_t launch_v(const KernelTables &t, const int16_t *d_in, int nblk, const 
     const int nframes = nblk * FRAMES;
     const long long items = (long long)nframes * ((nch + CHUNK - 1) / CHUNK);
     const int grid = (int)(items < (long long)g_cus * occ ? items : (long long)g_cus * occ);
-    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), 0, s, reinterpret_cast<const int *>(d_in),
-                       reinterpret_cast<float2 *>(d_out), stride_floats / 2, nframes, d_tunebins, nch,
-                       t.tw_p1, t.rec_f, t.post8192, t.hsel[D]);
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), 0, s, reinterpret_cast<const int *>(d_in), d_out,
+                       stride / 2, nframes, d_tunebins, nch, t.tw_p1, t.rec_f, t.post8192, t.hsel[D], oa);
     return hipGetLastError();
 }
 
 template <int D>
 hipError_t launch_d(const KernelTables &t, const int16_t *d_in, int nblk, const int *d_tunebins, int nch,
-                    float *d_out, size_t stride_floats, int lsb, int rand, int device, hipStream_t s)
+                    void *d_out, size_t stride, OutArgs oa, int rand, int cs16, int device, hipStream_t s)
 {
     if (rand)
-        return lsb ? launch_v<D, true, true>(t, d_in, nblk, d_tunebins, nch, d_out, stride_floats, device, s)
-                   : launch_v<D, true, false>(t, d_in, nblk, d_tunebins, nch, d_out, stride_floats, device, s);
-    return lsb ? launch_v<D, false, true>(t, d_in, nblk, d_tunebins, nch, d_out, stride_floats, device, s)
-               : launch_v<D, false, false>(t, d_in, nblk, d_tunebins, nch, d_out, stride_floats, device, s);
+        return cs16 ? launch_v<D, true, true>(t, d_in, nblk, d_tunebins, nch, d_out, stride, oa, device, s)
+                    : launch_v<D, true, false>(t, d_in, nblk, d_tunebins, nch, d_out, stride, oa, device, s);
+    return cs16 ? launch_v<D, false, true>(t, d_in, nblk, d_tunebins, nch, d_out, stride, oa, device, s)
+                : launch_v<D, false, false>(t, d_in, nblk, d_tunebins, nch, d_out, stride, oa, device, s);
 }
 
 }  // namespace
 
 hipError_t launch_channels_v2(const KernelTables &t, int d, const int16_t *d_in, int nblk, const int *d_tunebins,
-                              int nch, float *d_out, size_t stride_floats, int lsb, int rand, int device,
-                              hipStream_t s)
+                              int nch, void *d_out, size_t stride, int lsb, int rand, int cs16, float cs16_scale,
+                              int device, hipStream_t s)
 {
+    const OutArgs oa{lsb ? 0x80000000u : 0u, cs16_scale};
     switch (d) {
-    case 4: return launch_d<4>(t, d_in, nblk, d_tunebins, nch, d_out, stride_floats, lsb, rand, device, s);
-    case 5: return launch_d<5>(t, d_in, nblk, d_tunebins, nch, d_out, stride_floats, lsb, rand, device, s);
-    case 6: return launch_d<6>(t, d_in, nblk, d_tunebins, nch, d_out, stride_floats, lsb, rand, device, s);
+    case 4: return launch_d<4>(t, d_in, nblk, d_tunebins, nch, d_out, stride, oa, rand, cs16, device, s);
+    case 5: return launch_d<5>(t, d_in, nblk, d_tunebins, nch, d_out, stride, oa, rand, cs16, device, s);
+    case 6: return launch_d<6>(t, d_in, nblk, d_tunebins, nch, d_out, stride, oa, rand, cs16, device, s);
     default: return hipErrorInvalidValue;
     }
 }

@@ -31,21 +31,23 @@ hipError_t launch_frames(const KernelTables &t, int d, const int16_t *d_in, int 
 // v2 (default): persistent workgroups, input prefetch, swizzled LDS.  pq: the split x filter
 // coefficients of (d, tunebin), HALF >> d float4, built by launch_build_split_filter.
 // nco_starts/nco_trig: fused fine-tune NCO tables (fine_tune.h), or nullptr for none.
+// cs16: write saturate(rint(x * cs16_scale)) int16 (I, Q) pairs instead of complex float.
 hipError_t launch_frames_persistent(const KernelTables &t, int d, const int16_t *d_in, int nblk,
-                                    float *d_out, const float4 *pq, int tunebin, int lsb, int rand,
-                                    const float2 *nco_starts, const float2 *nco_trig, int device,
-                                    hipStream_t s);
+                                    void *d_out, const float4 *pq, int tunebin, int lsb, int rand,
+                                    int cs16, float cs16_scale, const float2 *nco_starts,
+                                    const float2 *nco_trig, int device, hipStream_t s);
 hipError_t launch_build_split_filter(const KernelTables &t, int d, int tunebin, float4 *pq, hipStream_t s);
 
 int channels_per_group(int d, int nch);
 
 // many-channel v2 (d = 4..6): persistent, forward once per (frame, 128-channel chunk)
+// stride: scalar components (float or int16) per channel row; cs16 as above
 hipError_t launch_channels_v2(const KernelTables &t, int d, const int16_t *d_in, int nblk, const int *d_tunebins,
-                              int nch, float *d_out, size_t stride_floats, int lsb, int rand, int device,
-                              hipStream_t s);
+                              int nch, void *d_out, size_t stride, int lsb, int rand, int cs16, float cs16_scale,
+                              int device, hipStream_t s);
 
 hipError_t launch_channels(const KernelTables &t, int d, const int16_t *d_in, int nblk,
-                           const int *d_tunebins, int nch, float *d_out, size_t stride_floats,
-                           int lsb, int rand, hipStream_t s);
+                           const int *d_tunebins, int nch, void *d_out, size_t stride,
+                           int lsb, int rand, int cs16, float cs16_scale, hipStream_t s);
 
 }  // namespace sddc

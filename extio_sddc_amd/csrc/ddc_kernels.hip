@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include "fft_device.hpp"
+#include "ddc_device_io.hpp"
 #include "ddc_kernels.h"
 
 namespace sddc {
@@ -157,6 +158,25 @@ __device__ __forceinline__ void emit_sample(float2 *__restrict__ out_blk, int k,
     }
 }
 
+// the same into a CF32 or CS16 stream (many-channel v1 path)
+template <int N>
+__device__ __forceinline__ void emit_sample_fmt(char *__restrict__ ob, int cs16, float scale, int k, int n,
+                                                float2 v, float conj_sign)
+{
+    v.y *= conj_sign;
+    int idx = -1;
+    if (k == 0) {
+        if (n >= N / 4 && n < 3 * N / 4) idx = n - N / 4;
+    } else if (n < 3 * N / 4) {
+        idx = N / 2 + (3 * N / 4) * (k - 1) + n;
+    }
+    if (idx < 0) return;
+    if (cs16)
+        reinterpret_cast<unsigned *>(ob)[idx] = cs16_pack(v, scale);
+    else
+        reinterpret_cast<float2 *>(ob)[idx] = v;
+}
+
 // ---------------------------------------------------------------------------
 // Single-channel fused frame kernel.  grid = nblk * 11 workgroups.
 //   in32 : int16 pairs of [history 4096 | nblk * 65536]
@@ -190,16 +210,17 @@ __global__ __launch_bounds__(kNT) void r2iq_frame_kernel(const int *__restrict__
 // Many-channel kernel: one workgroup per (frame, channel group).  The forward
 // transform is computed once per workgroup and shared by `cpg` channels
 // (SURVEY.md §8(e)): per channel the shift x H, the inverse and the write.
-//   out: channel c's stream at out + c*stride (float2 units)
+//   out: channel c's stream at complex element c*stride, CF32 or (cs16) int16 pairs
 // ---------------------------------------------------------------------------
 template <int D>
 __global__ __launch_bounds__(kNT) void r2iq_channels_kernel(const int *__restrict__ in32,
-                                                            float2 *__restrict__ out, size_t stride,
+                                                            void *__restrict__ out, size_t stride,
                                                             const float2 *__restrict__ tw4096,
                                                             const float2 *__restrict__ post8192,
                                                             const float2 *__restrict__ hsel,
                                                             const int *__restrict__ tunebins,
-                                                            int nch, int cpg, int lsb, int rand)
+                                                            int nch, int cpg, int lsb, int rand,
+                                                            int cs16, float cs16_scale)
 {
     constexpr int N = kHalf >> D;
     __shared__ float2 zbuf[lds_slots(kHalf)];
@@ -215,11 +236,11 @@ __global__ __launch_bounds__(kNT) void r2iq_channels_kernel(const int *__restric
     const int c0 = (int)blockIdx.y * cpg;
     for (int c = c0; c < c0 + cpg && c < nch; c++) {
         const int tb = tunebins[c];
-        float2 *out_blk = out + (size_t)c * stride + (size_t)blk * 8 * N;
+        char *ob = static_cast<char *>(out) + ((size_t)c * stride + (size_t)blk * 8 * N) * (cs16 ? 4 : 8);
         // first inverse pass reads Z from zbuf; the rest run in `work`
         auto ldsload = [&](int n) { return work[lds_pad(n)]; };
         auto ldsstore = [&](int pos, float2 v) { work[lds_pad(pos)] = v; };
-        auto emit = [&](int n, float2 v) { emit_sample<N>(out_blk, k, n, v, cs); };
+        auto emit = [&](int n, float2 v) { emit_sample_fmt<N>(ob, cs16, cs16_scale, k, n, v, cs); };
         auto binload = [&](int m) { return shifted_bin<N>(zbuf, m, tb, post8192, hsel); };
         if constexpr (N >= 512) {
             constexpr int R0 = N / 256;
@@ -294,14 +315,14 @@ hipError_t launch_frames(const KernelTables &t, int d, const int16_t *d_in, int 
 
 template <int D>
 static hipError_t launch_channels_d(const KernelTables &t, const int16_t *d_in, int nblk,
-                                    const int *d_tunebins, int nch, float *d_out, size_t stride_floats,
-                                    int lsb, int rand, hipStream_t s)
+                                    const int *d_tunebins, int nch, void *d_out, size_t stride,
+                                    int lsb, int rand, int cs16, float cs16_scale, hipStream_t s)
 {
     const int cpg = channels_per_group(D, nch);
     dim3 grid((unsigned)(nblk * kFrames), (unsigned)((nch + cpg - 1) / cpg)), block(kNT);
-    hipLaunchKernelGGL(r2iq_channels_kernel<D>, grid, block, 0, s,
-                       reinterpret_cast<const int *>(d_in), reinterpret_cast<float2 *>(d_out),
-                       stride_floats / 2, t.tw4096, t.post8192, t.hsel[D], d_tunebins, nch, cpg, lsb, rand);
+    hipLaunchKernelGGL(r2iq_channels_kernel<D>, grid, block, 0, s, reinterpret_cast<const int *>(d_in), d_out,
+                       stride / 2, t.tw4096, t.post8192, t.hsel[D], d_tunebins, nch, cpg, lsb, rand, cs16,
+                       cs16_scale);
     return hipGetLastError();
 }
 
@@ -314,19 +335,21 @@ int channels_per_group(int d, int nch)
 }
 
 hipError_t launch_channels(const KernelTables &t, int d, const int16_t *d_in, int nblk,
-                           const int *d_tunebins, int nch, float *d_out, size_t stride_floats,
-                           int lsb, int rand, hipStream_t s)
+                           const int *d_tunebins, int nch, void *d_out, size_t stride,
+                           int lsb, int rand, int cs16, float cs16_scale, hipStream_t s)
 {
+#define SDDC_CH(D) launch_channels_d<D>(t, d_in, nblk, d_tunebins, nch, d_out, stride, lsb, rand, cs16, cs16_scale, s)
     switch (d) {
-    case 0: return launch_channels_d<0>(t, d_in, nblk, d_tunebins, nch, d_out, stride_floats, lsb, rand, s);
-    case 1: return launch_channels_d<1>(t, d_in, nblk, d_tunebins, nch, d_out, stride_floats, lsb, rand, s);
-    case 2: return launch_channels_d<2>(t, d_in, nblk, d_tunebins, nch, d_out, stride_floats, lsb, rand, s);
-    case 3: return launch_channels_d<3>(t, d_in, nblk, d_tunebins, nch, d_out, stride_floats, lsb, rand, s);
-    case 4: return launch_channels_d<4>(t, d_in, nblk, d_tunebins, nch, d_out, stride_floats, lsb, rand, s);
-    case 5: return launch_channels_d<5>(t, d_in, nblk, d_tunebins, nch, d_out, stride_floats, lsb, rand, s);
-    case 6: return launch_channels_d<6>(t, d_in, nblk, d_tunebins, nch, d_out, stride_floats, lsb, rand, s);
+    case 0: return SDDC_CH(0);
+    case 1: return SDDC_CH(1);
+    case 2: return SDDC_CH(2);
+    case 3: return SDDC_CH(3);
+    case 4: return SDDC_CH(4);
+    case 5: return SDDC_CH(5);
+    case 6: return SDDC_CH(6);
     default: return hipErrorInvalidValue;
     }
+#undef SDDC_CH
 }
 
 }  // namespace sddc

@@ -20,6 +20,7 @@
 
 #include "ddc_kernels.h"
 #include "fft_device.hpp"
+#include "ddc_device_io.hpp"
 
 namespace sddc {
 namespace {
@@ -46,9 +47,6 @@ constexpr bool kDB = SDDC_DB != 0;
 #endif
 #ifndef SDDC_PQ
 #define SDDC_PQ 1             // split x filter from the per-(d, tunebin) coefficient table (P, Q)
-#endif
-#ifndef SDDC_BUF
-#define SDDC_BUF 1            // buffer loads/stores (SGPR base + offsets, no per-access VALU address math)
 #endif
 #ifndef SDDC_PREFETCH
 #define SDDC_PREFETCH 1       // load the next frame's input during the current one
@@ -140,33 +138,6 @@ __device__ __forceinline__ float2 split_bin(const float2 *lds, int bin, float2 w
     return cmul(cadd(A, cmul(Bi, wbin)), hh);
 }
 
-// Raw buffer access: a wave-uniform base (SGPRs), a per-thread byte offset and a uniform
-// byte offset (SGPR or immediate), so per-access address arithmetic is scalar.
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void *base)
-{
-    // raw (stride 0) buffer, byte range checked against 2^31 - 1; dword3 for gfx950
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, 0x7fffffff, 0x00020000);
-}
-__device__ __forceinline__ float4 buf_load16(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff)
-{
-    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0);
-    return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
-}
-__device__ __forceinline__ int buf_load4(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff)
-{
-    return (int)__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0);
-}
-__device__ __forceinline__ void buf_store8(float2 v, __amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff)
-{
-    u32x2 u;
-    u.x = __float_as_uint(v.x);
-    u.y = __float_as_uint(v.y);
-    __builtin_amdgcn_raw_buffer_store_b64(u, r, voff, soff, 0);
-}
-
 // Frame k of a block: output base of the kept samples, relative to the block's output
 template <int N>
 __device__ __forceinline__ int emit_base(int k)
@@ -174,86 +145,39 @@ __device__ __forceinline__ int emit_base(int k)
     return k == 0 ? -N / 4 : N / 2 + (3 * N / 4) * (k - 1);
 }
 
-template <int N, bool LSB>
-__device__ __forceinline__ void emit(float2 *__restrict__ out_blk, int k, int n, float2 v)
-{
-    if constexpr (LSB) v.y = -v.y;   // copy<flip=true>, fft_mt_r2iq.h:63-71
-    if (k == 0)
-        out_blk[n - N / 4] = v;
-    else
-        out_blk[N / 2 + (3 * N / 4) * (k - 1) + n] = v;
-}
-
-// Fine-tune NCO on output sample o of the batch (fine_tune.h): phasor T[q-1] * S_b[l] for
-// o = 128 b + 4 q + l, then the mix, in pf_mixer.cpp:808-833's float operation order.
-struct NcoArgs {
-    const float2 *starts;   // [blocks][4] lane starts of this batch (host chain)
-    const float2 *trig;     // [32] T
-};
-
-__device__ __forceinline__ float2 nco_mix(float2 v, const NcoArgs &nco, int o)
-{
-#pragma clang fp contract(off)
-    const float2 sb = nco.starts[(o >> 7) * 4 + (o & 3)];
-    const int q = (o >> 2) & 31;
-    const float2 tq = nco.trig[(q + 31) & 31];   // T[q-1]; unused for q = 0
-    const float2 pq = make_float2(tq.x * sb.x - tq.y * sb.y, tq.y * sb.x + tq.x * sb.y);
-    const float2 p = q ? pq : sb;
-    return make_float2(v.x * p.x - v.y * p.y, v.y * p.x + v.x * p.y);
-}
-
 // The kept outputs n = t + NB r of frame k (r in [4, 12) for k = 0, [0, 12) otherwise).
-// obase: the frame's first output slot relative to the batch (for the NCO).
-template <int N, int NB, bool LSB, bool NCO>
-__device__ __forceinline__ void emit_frame(float2 *__restrict__ out_blk, int k, int t, const float2 (&u)[16],
-                                           const NcoArgs &nco, int obase)
+// fbase: the frame's first kept output slot relative to the batch (also the NCO index).
+template <int NB, bool NCO, bool CS16>
+__device__ __forceinline__ void emit_frame(void *__restrict__ out, int fbase, int k, int t, const float2 (&u)[16],
+                                           const OutArgs &oa, const NcoArgs &nco)
 {
-    if constexpr (SDDC_BUF) {
-        const __amdgpu_buffer_rsrc_t ro = buf_rsrc(out_blk + emit_base<N>(k));
-        const unsigned vo = 8u * (unsigned)t;
-        const int r0 = k == 0 ? 4 : 0;   // wave-uniform
+    const __amdgpu_buffer_rsrc_t ro = buf_rsrc(static_cast<char *>(out) + (size_t)fbase * out_bytes<CS16>());
+    const int r0 = k == 0 ? 4 : 0;   // wave-uniform
 #pragma unroll
-        for (int r = 0; r < 12; r++) {
-            if (r < r0) continue;
-            float2 v = u[r];
-            if constexpr (LSB) v.y = -v.y;   // copy<flip=true>, fft_mt_r2iq.h:63-71
-            if constexpr (NCO) v = nco_mix(v, nco, obase + t + NB * r);
-            buf_store8(v, ro, vo, 8u * NB * r);
-        }
-        return;
-    }
-    static_assert(SDDC_BUF || !NCO, "the fused NCO needs the buffer-store output stage");
-    if (k == 0) {
-#pragma unroll
-        for (int r = 4; r < 12; r++) emit<N, LSB>(out_blk, 0, t + NB * r, u[r]);
-    } else {
-#pragma unroll
-        for (int r = 0; r < 12; r++) emit<N, LSB>(out_blk, k, t + NB * r, u[r]);
+    for (int r = 0; r < 12; r++) {
+        if (r < r0) continue;
+        float2 v = flip(u[r], oa.lsbmask);
+        if constexpr (NCO) v = nco_mix(v, nco, fbase + t + NB * r);
+        store_iq<CS16>(v, ro, (unsigned)t, (unsigned)(NB * r), oa);
     }
 }
 
 __device__ __forceinline__ void load_frame(const int *__restrict__ in32, int blk, int k, int (&x)[16])
 {
-    if constexpr (SDDC_BUF) {
-        const __amdgpu_buffer_rsrc_t rs = buf_rsrc(in32 + ((size_t)blk * BLOCK + (size_t)k * HOP) / 2);
-        const unsigned vo = 4u * threadIdx.x;
+    const __amdgpu_buffer_rsrc_t rs = buf_rsrc(in32 + ((size_t)blk * BLOCK + (size_t)k * HOP) / 2);
+    const unsigned vo = 4u * threadIdx.x;
 #pragma unroll
-        for (int r = 0; r < 16; r++) x[r] = buf_load4(rs, vo, 4u * NT * r);
-        return;
-    }
-    const int *p = in32 + ((size_t)blk * BLOCK + (size_t)k * HOP) / 2 + threadIdx.x;
-#pragma unroll
-    for (int r = 0; r < 16; r++) x[r] = p[NT * r];
+    for (int r = 0; r < 16; r++) x[r] = buf_load4(rs, vo, 4u * NT * r);
 }
 
-template <int D, bool RAND, bool LSB, bool NCO>
+template <int D, bool RAND, bool NCO, bool CS16>
 __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
-    const int *__restrict__ in32, float2 *__restrict__ out, int nframes,
+    const int *__restrict__ in32, void *__restrict__ out, int nframes,
     const float2 *__restrict__ tw_p1, const float2 *__restrict__ tw_q1,
     const float2 *__restrict__ rec_f, const float2 *__restrict__ rec_i,
     const float2 *__restrict__ twt_f, const float2 *__restrict__ twt_i,
     const float2 *__restrict__ post8192, const float2 *__restrict__ hsel,
-    const float4 *__restrict__ pq, int tunebin, NcoArgs nco)
+    const float4 *__restrict__ pq, int tunebin, OutArgs oa, NcoArgs nco)
 {
     constexpr int N = HALF >> D;
     __shared__ __attribute__((aligned(16))) float2 lds[kDB ? 2 * HALF : HALF];
@@ -299,8 +223,7 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
         asm volatile("" : "+v"(fw1), "+v"(fw4), "+v"(iw1), "+v"(iw4), "+v"(pb));
         const int sT = swz(t);            // swz(t + 256 r) = sT + 256 r
         const int x15 = t & 15;
-        float2 *out_blk = out + (size_t)blk * 8 * N;
-        const int oblk = blk * 8 * N;   // NCO sample index of the block (batch-relative)
+        const int oblk = blk * 8 * N;   // first output slot of the block (batch-relative)
         const int kc = k;
         // ---- forward pass 0 (R16, NS1): convert + DFT16 from registers ----
         float2 v[16];
@@ -384,10 +307,8 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
                         float4 c;
                         if constexpr (SDDC_FAKE & 1)
                             c = make_float4(0.5f, 0.25f * r, 0.1f, 0.2f);
-                        else if constexpr (SDDC_BUF)
-                            c = buf_load16(rpq, tb16, 16u * NT * r);
                         else
-                            c = *reinterpret_cast<const float4 *>(reinterpret_cast<const char *>(pqz + NT * r) + tb16);
+                            c = buf_load16(rpq, tb16, 16u * NT * r);
                         a[r] = split_pq(zk, zc, c);
                         continue;
                     }
@@ -461,7 +382,7 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
                     twiddle_rec16<+1>(a, iw1, iw4);
                 }
                 dft16<+1>(a, u);
-                emit_frame<N, NB, LSB, NCO>(out_blk, kc, t, u, nco, oblk + emit_base<N>(kc));
+                emit_frame<NB, NCO, CS16>(out, oblk + emit_base<N>(kc), kc, t, u, oa, nco);
             }
         } else {
             // ---- N <= 256: materialise the N filtered bins, then [N/16, 16] ----
@@ -499,7 +420,7 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
 #pragma unroll
                 for (int r = 1; r < 16; r++) a[r] = cmulc(a[r], twl[15 * 16 + (r - 1) * NB + t]);
                 dft16<+1>(a, u);
-                emit_frame<N, NB, LSB, NCO>(out_blk, kc, t, u, nco, oblk + emit_base<N>(kc));
+                emit_frame<NB, NCO, CS16>(out, oblk + emit_base<N>(kc), kc, t, u, oa, nco);
             }
         }
         if constexpr (kDB) {   // the next frame writes the buffer this frame's last pass did not read
@@ -539,19 +460,20 @@ int g_cus = 0;
 struct Launch {
     const int16_t *d_in;
     int nblk;
-    float *d_out;
+    void *d_out;
     const float4 *pq;
     int tunebin;
     int device;
     hipStream_t s;
+    OutArgs oa;
     NcoArgs nco;
 };
 
-template <int D, bool RAND, bool LSB, bool NCO>
+template <int D, bool RAND, bool NCO, bool CS16>
 hipError_t launch_v(const KernelTables &t, const Launch &L)
 {
-    auto kern = r2iq_persistent_kernel<D, RAND, LSB, NCO>;
-    int &occ = g_occupancy[D][(RAND ? 4 : 0) + (LSB ? 2 : 0) + (NCO ? 1 : 0)];
+    auto kern = r2iq_persistent_kernel<D, RAND, NCO, CS16>;
+    int &occ = g_occupancy[D][(RAND ? 4 : 0) + (NCO ? 2 : 0) + (CS16 ? 1 : 0)];
     if (occ == 0) {
         int nb = 0;
         hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, NT, 0);
@@ -566,22 +488,23 @@ hipError_t launch_v(const KernelTables &t, const Launch &L)
     int grid = g_cus * occ;
     if (grid > nframes) grid = nframes;
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), 0, L.s, reinterpret_cast<const int *>(L.d_in),
-                       reinterpret_cast<float2 *>(L.d_out), nframes, t.tw_p1, t.tw_q1[D], t.rec_f, t.rec_i[D],
-                       t.twt_f, t.twt_i[D], t.post8192, t.hsel[D], L.pq, L.tunebin, L.nco);
+                       L.d_out, nframes, t.tw_p1, t.tw_q1[D], t.rec_f, t.rec_i[D], t.twt_f, t.twt_i[D],
+                       t.post8192, t.hsel[D], L.pq, L.tunebin, L.oa, L.nco);
     return hipGetLastError();
 }
 
-template <int D, bool RAND, bool LSB>
-hipError_t launch_n(const KernelTables &t, const Launch &L)
+template <int D, bool RAND, bool NCO>
+hipError_t launch_f(const KernelTables &t, const Launch &L, bool cs16)
 {
-    return L.nco.starts ? launch_v<D, RAND, LSB, true>(t, L) : launch_v<D, RAND, LSB, false>(t, L);
+    return cs16 ? launch_v<D, RAND, NCO, true>(t, L) : launch_v<D, RAND, NCO, false>(t, L);
 }
 
 template <int D>
-hipError_t launch_d(const KernelTables &t, const Launch &L, int lsb, int rand)
+hipError_t launch_d(const KernelTables &t, const Launch &L, int rand, bool cs16)
 {
-    if (rand) return lsb ? launch_n<D, true, true>(t, L) : launch_n<D, true, false>(t, L);
-    return lsb ? launch_n<D, false, true>(t, L) : launch_n<D, false, false>(t, L);
+    const bool nco = L.nco.starts != nullptr;
+    if (rand) return nco ? launch_f<D, true, true>(t, L, cs16) : launch_f<D, true, false>(t, L, cs16);
+    return nco ? launch_f<D, false, true>(t, L, cs16) : launch_f<D, false, false>(t, L, cs16);
 }
 
 }  // namespace
@@ -595,19 +518,21 @@ hipError_t launch_build_split_filter(const KernelTables &t, int d, int tunebin, 
     return hipGetLastError();
 }
 
-hipError_t launch_frames_persistent(const KernelTables &t, int d, const int16_t *d_in, int nblk, float *d_out,
-                                    const float4 *pq, int tunebin, int lsb, int rand, const float2 *nco_starts,
-                                    const float2 *nco_trig, int device, hipStream_t s)
+hipError_t launch_frames_persistent(const KernelTables &t, int d, const int16_t *d_in, int nblk, void *d_out,
+                                    const float4 *pq, int tunebin, int lsb, int rand, int cs16, float cs16_scale,
+                                    const float2 *nco_starts, const float2 *nco_trig, int device, hipStream_t s)
 {
-    const Launch L{d_in, nblk, d_out, pq, tunebin, device, s, NcoArgs{nco_starts, nco_trig}};
+    const Launch L{d_in, nblk, d_out, pq, tunebin, device, s, OutArgs{lsb ? 0x80000000u : 0u, cs16_scale},
+                   NcoArgs{nco_starts, nco_trig}};
+    const bool f = cs16 != 0;
     switch (d) {
-    case 0: return launch_d<0>(t, L, lsb, rand);
-    case 1: return launch_d<1>(t, L, lsb, rand);
-    case 2: return launch_d<2>(t, L, lsb, rand);
-    case 3: return launch_d<3>(t, L, lsb, rand);
-    case 4: return launch_d<4>(t, L, lsb, rand);
-    case 5: return launch_d<5>(t, L, lsb, rand);
-    case 6: return launch_d<6>(t, L, lsb, rand);
+    case 0: return launch_d<0>(t, L, rand, f);
+    case 1: return launch_d<1>(t, L, rand, f);
+    case 2: return launch_d<2>(t, L, rand, f);
+    case 3: return launch_d<3>(t, L, rand, f);
+    case 4: return launch_d<4>(t, L, rand, f);
+    case 5: return launch_d<5>(t, L, rand, f);
+    case 6: return launch_d<6>(t, L, rand, f);
     default: return hipErrorInvalidValue;
     }
 }

@@ -74,6 +74,8 @@ struct sddc_ddc {
     float gain = 0.f;
     int d = 0, lsb = 0, rand = 0, tunebin = SDDC_DDC_HALF_FFT / 4;   // ctor: mtunebin = halfFft/4
     int variant = 0;                       // 0: persistent (v2), 1: one workgroup per frame (v1)
+    int out_fmt = SDDC_DDC_FMT_CF32;       // output stage format
+    float cs16_scale = 1.f;
     sddc::KernelTables tables;
     float2 *d_tables = nullptr;
 
@@ -369,11 +371,13 @@ static hipError_t stage_nco(sddc_ddc_t *h, int nblk, hipStream_t s)
     return hipEventRecord(h->nco_ev[slot], s);
 }
 
-static hipError_t launch_single(sddc_ddc_t *h, const int16_t *d_in, int nblk, float *d_out, hipStream_t s)
+static hipError_t launch_single(sddc_ddc_t *h, const int16_t *d_in, int nblk, void *d_out, hipStream_t s)
 {
     if (h->variant == 1) {
-        if (h->nco_fc != 0.f) return hipErrorNotSupported;   // the v1 reference variant has no NCO stage
-        return sddc::launch_frames(h->tables, h->d, d_in, nblk, d_out, h->tunebin, h->lsb, h->rand, s);
+        // the v1 reference variant has neither the NCO nor the CS16 stage
+        if (h->nco_fc != 0.f || h->out_fmt != SDDC_DDC_FMT_CF32) return hipErrorNotSupported;
+        return sddc::launch_frames(h->tables, h->d, d_in, nblk, static_cast<float *>(d_out), h->tunebin, h->lsb,
+                                   h->rand, s);
     }
     const bool nco = h->nco_fc != 0.f;
     if (nco) {
@@ -392,10 +396,24 @@ static hipError_t launch_single(sddc_ddc_t *h, const int16_t *d_in, int nblk, fl
     }
     hipError_t e = sddc::launch_frames_persistent(
         h->tables, h->d, d_in, nblk, d_out, h->d_pq, h->tunebin, h->lsb, h->rand,
-        nco ? h->d_nco + sddc::FineTune::kTable : nullptr, nco ? h->d_nco : nullptr, h->device, s);
+        h->out_fmt == SDDC_DDC_FMT_CS16, h->cs16_scale, nco ? h->d_nco + sddc::FineTune::kTable : nullptr,
+        nco ? h->d_nco : nullptr, h->device, s);
     if (e != hipSuccess) return e;
     h->pq_stream = s;
     return hipEventRecord(h->pq_used, s);
+}
+
+int sddc_ddc_set_output_format(sddc_ddc_t *h, int format, float cs16_scale)
+{
+    if (!h) return fail(SDDC_ERR_ARG, "null handle");
+    if (format != SDDC_DDC_FMT_CF32 && format != SDDC_DDC_FMT_CS16)
+        return fail(SDDC_ERR_ARG, "unknown output format %d", format);
+    if (format == SDDC_DDC_FMT_CS16 && !(std::isfinite(cs16_scale) && cs16_scale > 0.f))
+        return fail(SDDC_ERR_ARG, "CS16 scale must be finite and > 0");
+    std::lock_guard<std::mutex> lk(h->mu);
+    h->out_fmt = format;
+    h->cs16_scale = format == SDDC_DDC_FMT_CS16 ? cs16_scale : 1.f;
+    return SDDC_OK;
 }
 
 int sddc_ddc_set_fine_tune(sddc_ddc_t *h, float relative_freq)
@@ -424,11 +442,12 @@ static int check_process_args(sddc_ddc_t *h, const int16_t *in, int nblk, const 
     if (nblk <= 0) return fail(SDDC_ERR_ARG, "nblk must be > 0 (got %d)", nblk);
     if (!in || !out) return fail(SDDC_ERR_ARG, "null buffer");
     if (((uintptr_t)in & 3) != 0) return fail(SDDC_ERR_ARG, "input must be 4-byte aligned");
-    if (((uintptr_t)out & 7) != 0) return fail(SDDC_ERR_ARG, "output must be 8-byte aligned");
+    const unsigned oal = h->out_fmt == SDDC_DDC_FMT_CS16 ? 4 : 8;
+    if (((uintptr_t)out & (oal - 1)) != 0) return fail(SDDC_ERR_ARG, "output must be %u-byte aligned", oal);
     return SDDC_OK;
 }
 
-int sddc_ddc_process_device(sddc_ddc_t *h, const int16_t *d_in, int nblk, float *d_out, void *hip_stream)
+int sddc_ddc_process_device(sddc_ddc_t *h, const int16_t *d_in, int nblk, void *d_out, void *hip_stream)
 {
     int rc = check_process_args(h, d_in, nblk, d_out);
     if (rc) return rc;
@@ -440,7 +459,7 @@ int sddc_ddc_process_device(sddc_ddc_t *h, const int16_t *d_in, int nblk, float 
 }
 
 int sddc_ddc_process_channels_device(sddc_ddc_t *h, const int16_t *d_in, int nblk, const int *tunebins,
-                                     int nch, float *d_out, size_t out_stride_floats, void *hip_stream)
+                                     int nch, void *d_out, size_t out_stride, void *hip_stream)
 {
     int rc = check_process_args(h, d_in, nblk, d_out);
     if (rc) return rc;
@@ -451,8 +470,9 @@ int sddc_ddc_process_channels_device(sddc_ddc_t *h, const int16_t *d_in, int nbl
             return fail(SDDC_ERR_ARG, "channel %d tune bin %d outside [0,4096)", c, tunebins[c]);
     if (h->nco_fc != 0.f) return fail(SDDC_ERR_STATE, "fine-tune NCO is single-channel; set it to 0 first");
     const size_t need = (size_t)nblk * (size_t)(SDDC_DDC_OUT_BLOCK >> h->d) * 2;
-    if (nch > 1 && out_stride_floats < need)
-        return fail(SDDC_ERR_ARG, "out_stride_floats %zu < %zu floats per channel", out_stride_floats, need);
+    if (nch > 1 && out_stride < need)
+        return fail(SDDC_ERR_ARG, "out_stride %zu < %zu components per channel", out_stride, need);
+    const int cs16 = h->out_fmt == SDDC_DDC_FMT_CS16;
     DeviceGuard g(h->device);
     HIP_TRY(g.err);
     std::lock_guard<std::mutex> lk(h->mu);
@@ -465,15 +485,15 @@ int sddc_ddc_process_channels_device(sddc_ddc_t *h, const int16_t *d_in, int nbl
         HIP_TRY(hipMemcpy(h->d_tunebins, tunebins, nch * sizeof(int), hipMemcpyHostToDevice));
     }
     if (h->d >= 4 && h->variant == 0)
-        HIP_TRY(sddc::launch_channels_v2(h->tables, h->d, d_in, nblk, h->d_tunebins, nch, d_out,
-                                         out_stride_floats, h->lsb, h->rand, h->device, s));
+        HIP_TRY(sddc::launch_channels_v2(h->tables, h->d, d_in, nblk, h->d_tunebins, nch, d_out, out_stride,
+                                         h->lsb, h->rand, cs16, h->cs16_scale, h->device, s));
     else
-        HIP_TRY(sddc::launch_channels(h->tables, h->d, d_in, nblk, h->d_tunebins, nch, d_out,
-                                      out_stride_floats, h->lsb, h->rand, s));
+        HIP_TRY(sddc::launch_channels(h->tables, h->d, d_in, nblk, h->d_tunebins, nch, d_out, out_stride,
+                                      h->lsb, h->rand, cs16, h->cs16_scale, s));
     return SDDC_OK;
 }
 
-int sddc_ddc_process_host(sddc_ddc_t *h, const int16_t *in, int nblk, float *out)
+int sddc_ddc_process_host(sddc_ddc_t *h, const int16_t *in, int nblk, void *out)
 {
     int rc = check_process_args(h, in, nblk, out);
     if (rc) return rc;
@@ -481,25 +501,26 @@ int sddc_ddc_process_host(sddc_ddc_t *h, const int16_t *in, int nblk, float *out
     HIP_TRY(g.err);
     std::lock_guard<std::mutex> lk(h->mu);
     const size_t in_elems = kHistory + (size_t)kHostChunk * kBlock;
-    const size_t out_floats = (size_t)kHostChunk * SDDC_DDC_OUT_BLOCK * 2;
+    const size_t out_bytes_max = (size_t)kHostChunk * SDDC_DDC_OUT_BLOCK * 2 * sizeof(float);
     if (!h->h_in) {
         HIP_TRY(hipHostMalloc(&h->h_in, in_elems * sizeof(int16_t), hipHostMallocDefault));
         std::memset(h->h_in, 0, kHistory * sizeof(int16_t));
-        HIP_TRY(hipHostMalloc(&h->h_out, out_floats * sizeof(float), hipHostMallocDefault));
+        HIP_TRY(hipHostMalloc(&h->h_out, out_bytes_max, hipHostMallocDefault));
         HIP_TRY(hipMalloc(&h->d_in, in_elems * sizeof(int16_t)));
-        HIP_TRY(hipMalloc(&h->d_out, out_floats * sizeof(float)));
+        HIP_TRY(hipMalloc(&h->d_out, out_bytes_max));
     }
-    const int per_blk_out = (SDDC_DDC_OUT_BLOCK >> h->d) * 2;
+    // bytes of output per input block: (32768 >> d) complex samples, CF32 or CS16
+    const size_t per_blk_out = (size_t)(SDDC_DDC_OUT_BLOCK >> h->d) * (h->out_fmt == SDDC_DDC_FMT_CS16 ? 4 : 8);
+    char *outb = static_cast<char *>(out);
     for (int done = 0; done < nblk;) {
         const int n = std::min(kHostChunk, nblk - done);
         const size_t nin = kHistory + (size_t)n * kBlock;
         std::memcpy(h->h_in + kHistory, in + (size_t)done * kBlock, (size_t)n * kBlock * sizeof(int16_t));
         HIP_TRY(hipMemcpyAsync(h->d_in, h->h_in, nin * sizeof(int16_t), hipMemcpyHostToDevice, h->stream));
         HIP_TRY(launch_single(h, h->d_in, n, h->d_out, h->stream));
-        HIP_TRY(hipMemcpyAsync(h->h_out, h->d_out, (size_t)n * per_blk_out * sizeof(float),
-                               hipMemcpyDeviceToHost, h->stream));
+        HIP_TRY(hipMemcpyAsync(h->h_out, h->d_out, (size_t)n * per_blk_out, hipMemcpyDeviceToHost, h->stream));
         HIP_TRY(hipStreamSynchronize(h->stream));
-        std::memcpy(out + (size_t)done * per_blk_out, h->h_out, (size_t)n * per_blk_out * sizeof(float));
+        std::memcpy(outb + (size_t)done * per_blk_out, h->h_out, (size_t)n * per_blk_out);
         // keep the last 4096 samples as the next history (impl.hpp:32)
         std::memmove(h->h_in, h->h_in + (size_t)n * kBlock, kHistory * sizeof(int16_t));
         done += n;

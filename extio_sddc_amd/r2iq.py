@@ -24,6 +24,9 @@ import numpy as np
 from . import _lib
 from ._lib import DDCError, check
 
+FMT_CF32 = 0   # SDDC_DDC_FMT_CF32
+FMT_CS16 = 1   # SDDC_DDC_FMT_CS16
+
 HALF_FFT = 4096        # fft_mt_r2iq.h:18
 BLOCK = 65536          # config.h:80-81 transferSamples
 FRAMES = 11            # fft_mt_r2iq.h:19 fftPerBuf
@@ -76,6 +79,7 @@ class R2iq:
         self._d = 0
         self._rand = False
         self._lsb = False
+        self._fmt = FMT_CF32
 
     # -- lifecycle --------------------------------------------------------
     def close(self) -> None:
@@ -139,41 +143,55 @@ class R2iq:
         check(self._L.sddc_ddc_reset(self._h))
 
     # -- the hot loop -----------------------------------------------------
+    def setOutputFormat(self, fmt: str = "CF32", scale: float = 1.0) -> None:
+        """"CF32" (default, the reference's format) or "CS16": int16 (I, Q) =
+        saturate(rint(x * scale)) written by the kernels' output stage."""
+        code = {"CF32": FMT_CF32, "CS16": FMT_CS16}[fmt.upper()]
+        check(self._L.sddc_ddc_set_output_format(self._h, code, float(scale)))
+        self._fmt = code
+
+    def _out_dtype(self):
+        return np.int16 if self._fmt == FMT_CS16 else np.float32
+
     def process(self, blocks: np.ndarray) -> np.ndarray:
-        """Stateful host path: nblk blocks (int16) -> nblk*(32768>>d) complex64."""
+        """Stateful host path: nblk blocks (int16) -> nblk*(32768>>d) complex64
+        (CS16: an int16 array [n, 2])."""
         blocks = np.ascontiguousarray(blocks, np.int16).reshape(-1)
         if blocks.size % BLOCK:
             raise DDCError(-1, f"input length {blocks.size} is not a multiple of {BLOCK}")
         nblk = blocks.size // BLOCK
-        out = np.empty((output_samples(self._d, nblk), 2), np.float32)
+        out = np.empty((output_samples(self._d, nblk), 2), self._out_dtype())
         check(self._L.sddc_ddc_process_host(self._h, blocks.ctypes.data, nblk, out.ctypes.data))
+        if self._fmt == FMT_CS16:
+            return out
         return out.view(np.complex64).reshape(-1)
 
     def process_device(self, d_in, nblk: int, d_out, stream=None) -> None:
         """Stateless HBM path.  d_in: int16 device tensor [4096 + nblk*65536];
-        d_out: float32 device tensor [>= nblk*(32768>>d)*2].  Enqueued on `stream`
-        (a torch.cuda.Stream or raw handle; default: torch's current stream)."""
-        _check_device_buffers(d_in, nblk, d_out, output_samples(self._d, nblk) * 2)
+        d_out: float32 (CS16: int16) device tensor [>= nblk*(32768>>d)*2].  Enqueued on
+        `stream` (a torch.cuda.Stream or raw handle; default: torch's current stream)."""
+        _check_device_buffers(d_in, nblk, d_out, output_samples(self._d, nblk) * 2, self._fmt)
         check(self._L.sddc_ddc_process_device(self._h, d_in.data_ptr(), nblk, d_out.data_ptr(),
                                               _stream_handle(stream)))
 
     def process_channels_device(self, d_in, nblk: int, tunebins, d_out, stream=None) -> None:
-        """Many-channel path: d_out float32 [nch, nblk*(32768>>d)*2]."""
+        """Many-channel path: d_out float32 (CS16: int16) [nch, nblk*(32768>>d)*2]."""
         tb = np.ascontiguousarray(np.asarray(tunebins, np.int32))
         nch = tb.size
         per = output_samples(self._d, nblk) * 2
-        _check_device_buffers(d_in, nblk, d_out, per * nch)
+        _check_device_buffers(d_in, nblk, d_out, per * nch, self._fmt)
         stride = d_out.stride(0) if d_out.dim() > 1 else per
         check(self._L.sddc_ddc_process_channels_device(self._h, d_in.data_ptr(), nblk, tb.ctypes.data, nch,
                                                        d_out.data_ptr(), stride, _stream_handle(stream)))
 
 
-def _check_device_buffers(d_in, nblk, d_out, out_floats):
+def _check_device_buffers(d_in, nblk, d_out, out_floats, fmt=0):
     import torch
     if not (d_in.is_cuda and d_out.is_cuda):
         raise DDCError(-1, "device path needs device tensors")
-    if d_in.dtype != torch.int16 or d_out.dtype != torch.float32:
-        raise DDCError(-1, "d_in must be int16 and d_out float32")
+    want = torch.int16 if fmt == FMT_CS16 else torch.float32
+    if d_in.dtype != torch.int16 or d_out.dtype != want:
+        raise DDCError(-1, f"d_in must be int16 and d_out {want}")
     if not (d_in.is_contiguous() and d_out.is_contiguous()):
         raise DDCError(-1, "tensors must be contiguous")
     if d_in.numel() < HALF_FFT + nblk * BLOCK:

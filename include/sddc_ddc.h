@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define SDDC_DDC_ABI_VERSION 2   /* 2: + sddc_ddc_set_fine_tune */
+#define SDDC_DDC_ABI_VERSION 2   /* 2: + sddc_ddc_set_fine_tune, sddc_ddc_set_output_format */
 
 #define SDDC_DDC_HALF_FFT   4096    /* halfFft               fft_mt_r2iq.h:18 */
 #define SDDC_DDC_FFTN       8192    /* FFTN_R_ADC            config.h:49 */
@@ -110,29 +110,42 @@ int   sddc_ddc_set_fine_tune(sddc_ddc_t *h, float relative_freq);
 /* Complex samples produced per nblk input blocks at decimation d: nblk*(32768>>d). */
 size_t sddc_ddc_output_samples(int d, int nblk);
 
+/* ---- output format ---------------------------------- */
+/* CF32 (default): (I,Q) float pairs, the reference's output (RadioHandler / Soapy
+ * CF32, SoapySDDC/Streaming.cpp:12-50).  CS16: (I,Q) int16 pairs written by the
+ * kernels' output stage, value = saturate_int16(rint(x * cs16_scale)) with
+ * round-half-even; 4 bytes per complex sample instead of 8.  Applies to every
+ * process_* call (the NCO, if on, mixes first).  CS16 scale must be > 0. */
+#define SDDC_DDC_FMT_CF32 0
+#define SDDC_DDC_FMT_CS16 1
+int sddc_ddc_set_output_format(sddc_ddc_t *h, int format, float cs16_scale);
+
 /* ---- the hot loop (fft_mt_r2iq_impl.hpp:15-152) ---------------------------- */
-/* Device-resident; stateless apart from the fine-tune NCO phase.  d_in: device int16 [4096 + nblk*65536] = the
- * 4096-sample history followed by nblk blocks (2-byte aligned; 4-byte aligned
- * start required).  d_out: device float [nblk*(32768>>d)*2], (I,Q) pairs, in
- * stream order.  Uses the handle's d / sideband / rand / tunebin.  Enqueued on
- * `hip_stream` (a hipStream_t; NULL = default stream); returns after launch. */
+/* Device-resident; stateless apart from the fine-tune NCO phase.  d_in: device
+ * int16 [4096 + nblk*65536] = the 4096-sample history followed by nblk blocks
+ * (4-byte aligned start required).  d_out: device buffer of nblk*(32768>>d)
+ * complex samples in the output format (CF32: float (I,Q), 8-byte aligned;
+ * CS16: int16 (I,Q), 4-byte aligned), in stream order.  Uses the handle's
+ * d / sideband / rand / tunebin.  Enqueued on `hip_stream` (a hipStream_t;
+ * NULL = default stream); returns after launch. */
 int sddc_ddc_process_device(sddc_ddc_t *h, const int16_t *d_in, int nblk,
-                            float *d_out, void *hip_stream);
+                            void *d_out, void *hip_stream);
 
 /* Many-channel DDC: one forward transform per
  * frame, shared by `nch` channels with their own tune bins (host array, each a
- * multiple of 4 in [0,4096)).  d_out: channel c's stream starts at
- * d_out + c*out_stride_floats.  All channels use the handle's d/sideband/rand. */
+ * multiple of 4 in [0,4096)).  Channel c's stream starts `c*out_stride`
+ * components (floats for CF32, int16 for CS16; 2 per complex sample) into
+ * d_out.  All channels use the handle's d/sideband/rand/output format. */
 int sddc_ddc_process_channels_device(sddc_ddc_t *h, const int16_t *d_in, int nblk,
                                      const int *tunebins, int nch,
-                                     float *d_out, size_t out_stride_floats,
+                                     void *d_out, size_t out_stride,
                                      void *hip_stream);
 
 /* Stateful, host buffers: the r2iq worker body.  Consumes nblk consecutive
  * blocks from `in` (host int16 [nblk*65536]), keeps the 4096-sample history
  * across calls (zero after create/reset), writes nblk*(32768>>d) complex
- * samples to `out` (host float, (I,Q) pairs).  Synchronous. */
-int sddc_ddc_process_host(sddc_ddc_t *h, const int16_t *in, int nblk, float *out);
+ * samples to `out` (host, in the output format).  Synchronous. */
+int sddc_ddc_process_host(sddc_ddc_t *h, const int16_t *in, int nblk, void *out);
 
 #ifdef __cplusplus
 }
