@@ -46,6 +46,10 @@ SIGNATURES = {
     "sddc_ddc_process_device": (_I, [_P, _P, _I, _P, _P]),
     "sddc_ddc_process_channels_device": (_I, [_P, _P, _I, _P, _I, _P, _SZ, _P]),
     "sddc_ddc_process_host": (_I, [_P, _P, _I, _P]),
+    # include/sddc_fft.h
+    "sddc_fft_supported": (_I, [_I, _I]),
+    "sddc_fft_c2c": (_I, [_P, _P, _I, _I, _I, _P]),
+    "sddc_fft_r2c": (_I, [_P, _P, _I, _I, _P]),
 }
 
 ERRORS = {0: "SDDC_OK", -1: "SDDC_ERR_ARG", -2: "SDDC_ERR_HIP", -3: "SDDC_ERR_NODEV",

@@ -50,4 +50,10 @@ hipError_t launch_channels(const KernelTables &t, int d, const int16_t *d_in, in
                            const int *d_tunebins, int nch, void *d_out, size_t stride,
                            int lsb, int rand, int cs16, float cs16_scale, hipStream_t s);
 
+// batched FFTs (fft_batch.hip, include/sddc_fft.h); fft_prepare fills the device's twiddle
+// table once (synchronises s the first time)
+hipError_t fft_prepare(hipStream_t s);
+hipError_t fft_c2c(const void *in, void *out, int n, int batch, int dir, hipStream_t s);
+hipError_t fft_r2c(const float *in, void *out, int n, int batch, hipStream_t s);
+
 }  // namespace sddc

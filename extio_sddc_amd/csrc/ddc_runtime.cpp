@@ -20,6 +20,7 @@
 #include "ddc_kernels.h"
 #include "filterbank.h"
 #include "fine_tune.h"
+#include "sddc_fft.h"
 #include "sddc_ddc.h"
 #include "sddc_ddc_internal.h"
 
@@ -525,6 +526,39 @@ int sddc_ddc_process_host(sddc_ddc_t *h, const int16_t *in, int nblk, void *out)
         std::memmove(h->h_in, h->h_in + (size_t)n * kBlock, kHistory * sizeof(int16_t));
         done += n;
     }
+    return SDDC_OK;
+}
+
+/* ---- batched FFTs (include/sddc_fft.h) ------------------------------------ */
+int sddc_fft_supported(int kind, int n)
+{
+    const bool pow2 = n > 0 && (n & (n - 1)) == 0;
+    if (!pow2) return 0;
+    if (kind == 0) return n >= 64 && n <= 4096;
+    if (kind == 1) return n >= 128 && n <= 8192;
+    return 0;
+}
+
+int sddc_fft_c2c(const void *in, void *out, int n, int batch, int direction, void *hip_stream)
+{
+    if (!sddc_fft_supported(0, n)) return fail(SDDC_ERR_ARG, "c2c size %d unsupported (64..4096, power of 2)", n);
+    if (batch <= 0 || !in || !out) return fail(SDDC_ERR_ARG, "c2c: batch %d / null buffer", batch);
+    if (direction != SDDC_FFT_FORWARD && direction != SDDC_FFT_BACKWARD)
+        return fail(SDDC_ERR_ARG, "c2c: direction must be -1 or +1");
+    hipStream_t s = (hipStream_t)hip_stream;
+    HIP_TRY(sddc::fft_prepare(s));
+    HIP_TRY(sddc::fft_c2c(in, out, n, batch, direction, s));
+    return SDDC_OK;
+}
+
+int sddc_fft_r2c(const float *in, void *out, int n, int batch, void *hip_stream)
+{
+    if (!sddc_fft_supported(1, n)) return fail(SDDC_ERR_ARG, "r2c size %d unsupported (128..8192, power of 2)", n);
+    if (batch <= 0 || !in || !out) return fail(SDDC_ERR_ARG, "r2c: batch %d / null buffer", batch);
+    if (in == out) return fail(SDDC_ERR_ARG, "r2c: in place is not supported");
+    hipStream_t s = (hipStream_t)hip_stream;
+    HIP_TRY(sddc::fft_prepare(s));
+    HIP_TRY(sddc::fft_r2c(in, out, n, batch, s));
     return SDDC_OK;
 }
 

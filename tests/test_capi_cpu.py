@@ -13,12 +13,15 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "sddc_ddc.h")
+HEADERS = [HEADER, os.path.join(ROOT, "include", "sddc_fft.h")]
 
 
 def declared_symbols():
-    txt = open(HEADER).read()
-    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
-    return sorted(set(re.findall(r"\b(sddc_ddc_[a-z_0-9]+)\s*\(", txt)))
+    syms = set()
+    for h in HEADERS:
+        txt = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
+        syms |= set(re.findall(r"\b(sddc_(?:ddc|fft)_[a-z_0-9]+)\s*\(", txt))
+    return sorted(syms)
 
 
 def test_header_declares_expected_api():
@@ -32,7 +35,7 @@ def test_library_exports_every_declared_symbol(ddc_lib):
     import subprocess
     from extio_sddc_amd._lib import LIB_PATH, SIGNATURES
     out = subprocess.run(["nm", "-D", "--defined-only", LIB_PATH], capture_output=True, text=True).stdout
-    exported = set(re.findall(r" T (sddc_ddc_\w+)", out))
+    exported = set(re.findall(r" T (sddc_(?:ddc|fft)_\w+)", out))
     for s in declared_symbols():
         assert s in exported, s
         assert s in SIGNATURES, f"python binding lacks {s}"
