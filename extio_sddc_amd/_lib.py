@@ -46,6 +46,9 @@ SIGNATURES = {
     "sddc_ddc_process_device": (_I, [_P, _P, _I, _P, _P]),
     "sddc_ddc_process_channels_device": (_I, [_P, _P, _I, _P, _I, _P, _SZ, _P]),
     "sddc_ddc_process_host": (_I, [_P, _P, _I, _P]),
+    "sddc_ddc_process_blocks": (_I, [_P, _P, _I, _P]),
+    "sddc_ddc_register_host": (_I, [_P, _P, _SZ]),
+    "sddc_ddc_unregister_host": (_I, [_P, _P]),
     # include/sddc_fft.h
     "sddc_fft_supported": (_I, [_I, _I]),
     "sddc_fft_c2c": (_I, [_P, _P, _I, _I, _I, _P]),

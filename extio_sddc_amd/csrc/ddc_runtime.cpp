@@ -66,7 +66,8 @@ struct DeviceGuard {
 
 constexpr int kHistory = SDDC_DDC_HALF_FFT;
 constexpr int kBlock = SDDC_DDC_BLOCK;
-constexpr int kHostChunk = 64;   // blocks per H2D/kernel/D2H round on the host path
+constexpr int kHostChunk = 32;   // blocks per pipeline chunk on the host path
+constexpr size_t kOutBlockMax = (size_t)SDDC_DDC_OUT_BLOCK * 2 * sizeof(float);   // bytes, CF32 d = 0
 
 }  // namespace
 
@@ -81,11 +82,22 @@ struct sddc_ddc {
     float2 *d_tables = nullptr;
 
     std::mutex mu;                         // serialises the host path and buffer growth
-    hipStream_t stream = nullptr;          // host-path stream
-    int16_t *h_in = nullptr;               // pinned [history | chunk]
-    float *h_out = nullptr;                // pinned
-    int16_t *d_in = nullptr;
-    float *d_out = nullptr;
+    hipStream_t stream = nullptr;          // host path: compute stream
+
+    // host path pipeline (process_host / process_blocks): two chunk slots; H2D on s_in,
+    // kernel on `stream`, D2H on s_out, ordered by events.  The stream history (last 4096
+    // input samples) stays on the device: the tail of the newest slot's input.
+    struct HostSlot {
+        int16_t *d_in = nullptr;           // [history | kHostChunk blocks]
+        void *d_out = nullptr;
+        int16_t *h_in = nullptr;           // pinned staging, used for unregistered callers
+        void *h_out = nullptr;
+        hipEvent_t e_h2d = nullptr, e_k = nullptr, e_d2h = nullptr;
+    } hs[2];
+    hipStream_t s_in = nullptr, s_out = nullptr;
+    bool host_ready = false;
+    int last_slot = -1, last_n = 0;        // where the history lives; -1 = zeros (create/reset)
+    std::vector<std::pair<const char *, size_t>> regions;   // sddc_ddc_register_host
 
     int *d_tunebins = nullptr;             // channel tune bins (device)
     std::vector<int> tunebins_cached;
@@ -256,8 +268,17 @@ int sddc_ddc_destroy(sddc_ddc_t *h)
         DeviceGuard g(h->device);
         if (h->stream) (void)hipStreamSynchronize(h->stream);
         if (h->d_tables) (void)hipFree(h->d_tables);
-        if (h->d_in) (void)hipFree(h->d_in);
-        if (h->d_out) (void)hipFree(h->d_out);
+        for (auto &sl : h->hs) {
+            if (sl.d_in) (void)hipFree(sl.d_in);
+            if (sl.d_out) (void)hipFree(sl.d_out);
+            if (sl.h_in) (void)hipHostFree(sl.h_in);
+            if (sl.h_out) (void)hipHostFree(sl.h_out);
+            for (hipEvent_t ev : {sl.e_h2d, sl.e_k, sl.e_d2h})
+                if (ev) (void)hipEventDestroy(ev);
+        }
+        if (h->s_in) (void)hipStreamDestroy(h->s_in);
+        if (h->s_out) (void)hipStreamDestroy(h->s_out);
+        for (auto &r : h->regions) (void)hipHostUnregister(const_cast<char *>(r.first));
         if (h->d_tunebins) (void)hipFree(h->d_tunebins);
         if (h->d_pq) (void)hipFree(h->d_pq);
         if (h->pq_used) (void)hipEventDestroy(h->pq_used);
@@ -266,8 +287,6 @@ int sddc_ddc_destroy(sddc_ddc_t *h)
             if (h->nco_ev[i]) (void)hipEventDestroy(h->nco_ev[i]);
         }
         if (h->d_nco) (void)hipFree(h->d_nco);
-        if (h->h_in) (void)hipHostFree(h->h_in);
-        if (h->h_out) (void)hipHostFree(h->h_out);
         if (h->stream) (void)hipStreamDestroy(h->stream);
     }
     delete h;
@@ -326,7 +345,7 @@ int sddc_ddc_reset(sddc_ddc_t *h)
 {
     if (!h) return fail(SDDC_ERR_ARG, "null handle");
     std::lock_guard<std::mutex> lk(h->mu);
-    if (h->h_in) std::memset(h->h_in, 0, kHistory * sizeof(int16_t));
+    h->last_slot = -1;   // the next host-path chunk starts from a zero history
     return SDDC_OK;
 }
 
@@ -494,6 +513,124 @@ int sddc_ddc_process_channels_device(sddc_ddc_t *h, const int16_t *d_in, int nbl
     return SDDC_OK;
 }
 
+// ---- host path: pipelined chunks ------------------------------------------------------
+extern "C++" {
+
+static hipError_t host_setup(sddc_ddc_t *h)
+{
+    if (h->host_ready) return hipSuccess;
+    hipError_t e;
+    const size_t in_bytes = (kHistory + (size_t)kHostChunk * kBlock) * sizeof(int16_t);
+    const size_t out_bytes = (size_t)kHostChunk * kOutBlockMax;
+    for (auto &sl : h->hs) {
+        if ((e = hipMalloc(&sl.d_in, in_bytes)) != hipSuccess) return e;
+        if ((e = hipMalloc(&sl.d_out, out_bytes)) != hipSuccess) return e;
+        if ((e = hipHostMalloc(&sl.h_in, in_bytes, hipHostMallocDefault)) != hipSuccess) return e;
+        if ((e = hipHostMalloc(&sl.h_out, out_bytes, hipHostMallocDefault)) != hipSuccess) return e;
+        for (hipEvent_t *ev : {&sl.e_h2d, &sl.e_k, &sl.e_d2h})
+            if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess) return e;
+    }
+    if ((e = hipStreamCreateWithFlags(&h->s_in, hipStreamNonBlocking)) != hipSuccess) return e;
+    if ((e = hipStreamCreateWithFlags(&h->s_out, hipStreamNonBlocking)) != hipSuccess) return e;
+    h->host_ready = true;
+    return hipSuccess;
+}
+
+// true if [p, p + bytes) lies in memory registered through sddc_ddc_register_host
+static bool host_registered(const sddc_ddc_t *h, const void *p, size_t bytes)
+{
+    const char *c = static_cast<const char *>(p);
+    for (const auto &r : h->regions)
+        if (c >= r.first && c + bytes <= r.first + r.second) return true;
+    return false;
+}
+
+// nblk input blocks, block i at src(i) (host), output written contiguously to out.
+// Chunk k of kHostChunk blocks goes through slot k % 2:
+//   s_in   : wait e_k (kernel k-2 done with d_in) -> history D2D from the newest slot
+//            -> H2D of the blocks (direct from registered memory, else via h_in) -> e_h2d
+//   stream : wait e_h2d, e_d2h (D2H k-2 done with d_out) -> kernel -> e_k
+//   s_out  : wait e_k -> D2H (direct into registered memory, else into h_out) -> e_d2h
+// The host copies staged output of chunk k-1 while chunk k is in flight.
+template <class Src>
+static int host_pipeline(sddc_ddc_t *h, int nblk, Src src, void *out)
+{
+    HIP_TRY(host_setup(h));
+    // one chunk: nothing to overlap, so skip the cross-stream event hops
+    hipStream_t s_in = nblk <= kHostChunk ? h->stream : h->s_in;
+    hipStream_t s_out = nblk <= kHostChunk ? h->stream : h->s_out;
+    const size_t per_out = (size_t)(SDDC_DDC_OUT_BLOCK >> h->d) * (h->out_fmt == SDDC_DDC_FMT_CS16 ? 4 : 8);
+    const size_t blk_bytes = (size_t)kBlock * sizeof(int16_t);
+    char *outb = static_cast<char *>(out);
+    const bool out_direct = host_registered(h, out, (size_t)nblk * per_out);
+    int pend_slot = -1, pend_n = 0;        // staged output not yet copied to the caller
+    size_t pend_off = 0;
+    auto drain = [&]() -> int {
+        if (pend_slot < 0) return SDDC_OK;
+        HIP_TRY(hipEventSynchronize(h->hs[pend_slot].e_d2h));
+        std::memcpy(outb + pend_off, h->hs[pend_slot].h_out, (size_t)pend_n * per_out);
+        pend_slot = -1;
+        return SDDC_OK;
+    };
+    int slot = h->last_slot < 0 ? 0 : 1 - h->last_slot;
+    for (int done = 0; done < nblk; done += kHostChunk, slot ^= 1) {
+        const int n = std::min(kHostChunk, nblk - done);
+        auto &sl = h->hs[slot];
+        // ---- input: history, then the blocks ----
+        HIP_TRY(hipStreamWaitEvent(s_in, sl.e_k, 0));
+        if (h->last_slot < 0) {
+            HIP_TRY(hipMemsetAsync(sl.d_in, 0, kHistory * sizeof(int16_t), s_in));
+        } else {
+            const auto &prev = h->hs[h->last_slot];
+            HIP_TRY(hipMemcpyAsync(sl.d_in, prev.d_in + (size_t)h->last_n * kBlock, kHistory * sizeof(int16_t),
+                                   hipMemcpyDeviceToDevice, s_in));
+        }
+        bool staged_in = false;
+        for (int i = 0; i < n;) {
+            const int16_t *p = src(done + i);
+            int run = 1;   // merge blocks that are contiguous in host memory
+            while (i + run < n && src(done + i + run) == p + (size_t)run * kBlock) run++;
+            int16_t *dst = sl.d_in + kHistory + (size_t)i * kBlock;
+            if (host_registered(h, p, run * blk_bytes)) {
+                HIP_TRY(hipMemcpyAsync(dst, p, run * blk_bytes, hipMemcpyHostToDevice, s_in));
+            } else {
+                if (!staged_in) HIP_TRY(hipEventSynchronize(sl.e_h2d));   // h_in free again
+                staged_in = true;
+                std::memcpy(sl.h_in + (size_t)i * kBlock, p, run * blk_bytes);
+                HIP_TRY(hipMemcpyAsync(dst, sl.h_in + (size_t)i * kBlock, run * blk_bytes, hipMemcpyHostToDevice,
+                                       s_in));
+            }
+            i += run;
+        }
+        HIP_TRY(hipEventRecord(sl.e_h2d, s_in));
+        h->last_slot = slot;
+        h->last_n = n;
+        // ---- kernel ----
+        HIP_TRY(hipStreamWaitEvent(h->stream, sl.e_h2d, 0));
+        HIP_TRY(hipStreamWaitEvent(h->stream, sl.e_d2h, 0));
+        HIP_TRY(launch_single(h, sl.d_in, n, sl.d_out, h->stream));
+        HIP_TRY(hipEventRecord(sl.e_k, h->stream));
+        // ---- output ----
+        if (int rc = drain()) return rc;   // chunk k-1's staged output (its slot is reused next)
+        HIP_TRY(hipStreamWaitEvent(s_out, sl.e_k, 0));
+        if (out_direct) {
+            HIP_TRY(hipMemcpyAsync(outb + (size_t)done * per_out, sl.d_out, (size_t)n * per_out,
+                                   hipMemcpyDeviceToHost, s_out));
+        } else {
+            HIP_TRY(hipMemcpyAsync(sl.h_out, sl.d_out, (size_t)n * per_out, hipMemcpyDeviceToHost, s_out));
+            pend_slot = slot;
+            pend_n = n;
+            pend_off = (size_t)done * per_out;
+        }
+        HIP_TRY(hipEventRecord(sl.e_d2h, s_out));
+    }
+    if (int rc = drain()) return rc;
+    HIP_TRY(hipStreamSynchronize(s_out));
+    HIP_TRY(hipStreamSynchronize(s_in));   // callers may reuse their input buffers
+    return SDDC_OK;
+}
+}  // extern "C++"
+
 int sddc_ddc_process_host(sddc_ddc_t *h, const int16_t *in, int nblk, void *out)
 {
     int rc = check_process_args(h, in, nblk, out);
@@ -501,32 +638,51 @@ int sddc_ddc_process_host(sddc_ddc_t *h, const int16_t *in, int nblk, void *out)
     DeviceGuard g(h->device);
     HIP_TRY(g.err);
     std::lock_guard<std::mutex> lk(h->mu);
-    const size_t in_elems = kHistory + (size_t)kHostChunk * kBlock;
-    const size_t out_bytes_max = (size_t)kHostChunk * SDDC_DDC_OUT_BLOCK * 2 * sizeof(float);
-    if (!h->h_in) {
-        HIP_TRY(hipHostMalloc(&h->h_in, in_elems * sizeof(int16_t), hipHostMallocDefault));
-        std::memset(h->h_in, 0, kHistory * sizeof(int16_t));
-        HIP_TRY(hipHostMalloc(&h->h_out, out_bytes_max, hipHostMallocDefault));
-        HIP_TRY(hipMalloc(&h->d_in, in_elems * sizeof(int16_t)));
-        HIP_TRY(hipMalloc(&h->d_out, out_bytes_max));
-    }
-    // bytes of output per input block: (32768 >> d) complex samples, CF32 or CS16
-    const size_t per_blk_out = (size_t)(SDDC_DDC_OUT_BLOCK >> h->d) * (h->out_fmt == SDDC_DDC_FMT_CS16 ? 4 : 8);
-    char *outb = static_cast<char *>(out);
-    for (int done = 0; done < nblk;) {
-        const int n = std::min(kHostChunk, nblk - done);
-        const size_t nin = kHistory + (size_t)n * kBlock;
-        std::memcpy(h->h_in + kHistory, in + (size_t)done * kBlock, (size_t)n * kBlock * sizeof(int16_t));
-        HIP_TRY(hipMemcpyAsync(h->d_in, h->h_in, nin * sizeof(int16_t), hipMemcpyHostToDevice, h->stream));
-        HIP_TRY(launch_single(h, h->d_in, n, h->d_out, h->stream));
-        HIP_TRY(hipMemcpyAsync(h->h_out, h->d_out, (size_t)n * per_blk_out, hipMemcpyDeviceToHost, h->stream));
-        HIP_TRY(hipStreamSynchronize(h->stream));
-        std::memcpy(outb + (size_t)done * per_blk_out, h->h_out, (size_t)n * per_blk_out);
-        // keep the last 4096 samples as the next history (impl.hpp:32)
-        std::memmove(h->h_in, h->h_in + (size_t)n * kBlock, kHistory * sizeof(int16_t));
-        done += n;
-    }
+    return host_pipeline(h, nblk, [in](int i) { return in + (size_t)i * kBlock; }, out);
+}
+
+int sddc_ddc_process_blocks(sddc_ddc_t *h, const int16_t *const *blocks, int nblk, void *out)
+{
+    if (!blocks) return fail(SDDC_ERR_ARG, "null block list");
+    int rc = check_process_args(h, nblk > 0 ? blocks[0] : nullptr, nblk, out);
+    if (rc) return rc;
+    for (int i = 0; i < nblk; i++)
+        if (!blocks[i] || ((uintptr_t)blocks[i] & 3)) return fail(SDDC_ERR_ARG, "block %d null or unaligned", i);
+    DeviceGuard g(h->device);
+    HIP_TRY(g.err);
+    std::lock_guard<std::mutex> lk(h->mu);
+    return host_pipeline(h, nblk, [blocks](int i) { return blocks[i]; }, out);
+}
+
+int sddc_ddc_register_host(sddc_ddc_t *h, void *ptr, size_t bytes)
+{
+    if (!h || !ptr || !bytes) return fail(SDDC_ERR_ARG, "register_host: null handle/pointer or zero size");
+    DeviceGuard g(h->device);
+    HIP_TRY(g.err);
+    std::lock_guard<std::mutex> lk(h->mu);
+    for (const auto &r : h->regions)
+        if (static_cast<char *>(ptr) < r.first + r.second && r.first < static_cast<char *>(ptr) + bytes)
+            return fail(SDDC_ERR_ARG, "register_host: overlaps a registered region");
+    HIP_TRY(hipHostRegister(ptr, bytes, hipHostRegisterDefault));
+    h->regions.emplace_back(static_cast<const char *>(ptr), bytes);
     return SDDC_OK;
+}
+
+int sddc_ddc_unregister_host(sddc_ddc_t *h, void *ptr)
+{
+    if (!h || !ptr) return fail(SDDC_ERR_ARG, "unregister_host: null handle/pointer");
+    DeviceGuard g(h->device);
+    HIP_TRY(g.err);
+    std::lock_guard<std::mutex> lk(h->mu);
+    for (size_t i = 0; i < h->regions.size(); i++) {
+        if (h->regions[i].first == ptr) {
+            // in-flight host-path copies finished when process_* returned (synchronous)
+            HIP_TRY(hipHostUnregister(ptr));
+            h->regions.erase(h->regions.begin() + (long)i);
+            return SDDC_OK;
+        }
+    }
+    return fail(SDDC_ERR_ARG, "unregister_host: %p was not registered", ptr);
 }
 
 /* ---- batched FFTs (include/sddc_fft.h) ------------------------------------ */

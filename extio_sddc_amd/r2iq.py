@@ -166,6 +166,26 @@ class R2iq:
             return out
         return out.view(np.complex64).reshape(-1)
 
+    def process_blocks(self, blocks) -> np.ndarray:
+        """Host path over blocks scattered in memory (ring slots): a list of int16 arrays of
+        65536 samples each; same output and history semantics as process()."""
+        arrs = [np.ascontiguousarray(b, np.int16).reshape(-1) for b in blocks]
+        if any(a.size != BLOCK for a in arrs):
+            raise DDCError(-1, f"every block must hold {BLOCK} samples")
+        ptrs = (ctypes.c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])
+        out = np.empty((output_samples(self._d, len(arrs)), 2), self._out_dtype())
+        check(self._L.sddc_ddc_process_blocks(self._h, ptrs, len(arrs), out.ctypes.data))
+        if self._fmt == FMT_CS16:
+            return out
+        return out.view(np.complex64).reshape(-1)
+
+    def register_host(self, arr: np.ndarray) -> None:
+        """Pin a host array for direct DMA on the host path (unregister before freeing it)."""
+        check(self._L.sddc_ddc_register_host(self._h, arr.ctypes.data, arr.nbytes))
+
+    def unregister_host(self, arr: np.ndarray) -> None:
+        check(self._L.sddc_ddc_unregister_host(self._h, arr.ctypes.data))
+
     def process_device(self, d_in, nblk: int, d_out, stream=None) -> None:
         """Stateless HBM path.  d_in: int16 device tensor [4096 + nblk*65536];
         d_out: float32 (CS16: int16) device tensor [>= nblk*(32768>>d)*2].  Enqueued on

@@ -26,6 +26,8 @@
 #include <atomic>
 #include <cstdint>
 #include <string>
+#include <condition_variable>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -66,8 +68,16 @@ private:
     sddc_ddc *ddc_ = nullptr;         /* GPU handle (C ABI) */
     int device_ = 0;
     std::thread worker_;
-    std::vector<int16_t> in_stage_;   /* batched input blocks */
-    std::vector<float> out_stage_;    /* their IQ */
+    void writer();
+
+    /* batch IQ, double-buffered between the worker (GPU calls) and the writer thread
+     * (copies into the output ring, getWritePtr/WriteDone); registered with the library */
+    std::vector<float> out_stage_[2];
+    int stage_n_[2] = {0, 0};         /* blocks in a filled stage, 0 = free */
+    std::mutex stage_mu_;
+    std::condition_variable stage_cv_;
+    std::thread writer_;
+    void *in_region_ = nullptr;       /* input ring storage registered for direct DMA */
     std::atomic<uint64_t> blocks_done_{0};
     int wc_base_ = 0;                 /* input ring write count at TurnOn */
     uint64_t consumed_ = 0;           /* input blocks taken since TurnOn */

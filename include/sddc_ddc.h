@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define SDDC_DDC_ABI_VERSION 2   /* 2: + sddc_ddc_set_fine_tune, sddc_ddc_set_output_format */
+#define SDDC_DDC_ABI_VERSION 2   /* 2: + set_fine_tune, set_output_format, process_blocks, register_host */
 
 #define SDDC_DDC_HALF_FFT   4096    /* halfFft               fft_mt_r2iq.h:18 */
 #define SDDC_DDC_FFTN       8192    /* FFTN_R_ADC            config.h:49 */
@@ -146,6 +146,20 @@ int sddc_ddc_process_channels_device(sddc_ddc_t *h, const int16_t *d_in, int nbl
  * across calls (zero after create/reset), writes nblk*(32768>>d) complex
  * samples to `out` (host, in the output format).  Synchronous. */
 int sddc_ddc_process_host(sddc_ddc_t *h, const int16_t *in, int nblk, void *out);
+
+/* The same for blocks scattered in host memory (e.g. ring-buffer slots,
+ * Core/dsp/ringbuffer.h): block i is blocks[i] (65536 int16). */
+int sddc_ddc_process_blocks(sddc_ddc_t *h, const int16_t *const *blocks, int nblk,
+                            void *out);
+
+/* ---- ingest ---------------------------------------
+ * Pin a caller-owned host region (hipHostRegister) so the host path DMAs blocks
+ * from it and output into it directly instead of staging through the library's
+ * pinned buffers.  Regions must not overlap; unregister before freeing them.
+ * The host path runs chunks of 32 blocks through a two-slot pipeline (H2D,
+ * kernel and D2H on separate streams), whichever memory is used. */
+int sddc_ddc_register_host(sddc_ddc_t *h, void *ptr, size_t bytes);
+int sddc_ddc_unregister_host(sddc_ddc_t *h, void *ptr);
 
 #ifdef __cplusplus
 }
