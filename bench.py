@@ -35,10 +35,10 @@ BLOCK = 65536
 HALF = 4096
 
 
-def algorithmic_bytes_per_sample(d: int, nch: int = 1) -> float:
-    """B(d) = 2 B int16 read + 8 B per output complex / 2^(d+1) input samples, per channel
-    (SURVEY.md §8(d)); the 4/3 frame overlap and the tables are not counted."""
-    return 2.0 + nch * 8.0 / (1 << (d + 1))
+def algorithmic_bytes_per_sample(d: int, nch: int = 1, out_bytes: int = 8) -> float:
+    """B(d) = 2 B int16 read + one output complex (8 B CF32, 4 B CS16) per 2^(d+1) input
+    samples, per channel; the 4/3 frame overlap and the tables are not counted."""
+    return 2.0 + nch * float(out_bytes) / (1 << (d + 1))
 
 
 def make_input(torch, nblk: int, seed: int, device) -> "torch.Tensor":
@@ -113,6 +113,8 @@ def main() -> None:
     ap.add_argument("--channels", type=int, default=1024)
     ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds of CPU-baseline work")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cs16", type=float, default=0.0,
+                    help="CS16 output with this scale (int16 = rint(x * scale)); 0 = CF32")
     ap.add_argument("--fine-tune", type=float, default=0.0,
                     help="fused fine-tune NCO frequency (fraction of the output rate); 0 = off")
     args = ap.parse_args()
@@ -141,18 +143,25 @@ def main() -> None:
             raise SystemExit("--fine-tune is single-channel only")
         ddc.setFineTune(args.fine_tune)
         args.no_cpu_baseline = True   # the CPU leg is the plain DDC
+    out_bytes = 8
+    out_dtype = torch.float32
+    if args.cs16:
+        ddc.setOutputFormat("CS16", args.cs16)
+        out_bytes, out_dtype = 4, torch.int16
+        args.no_cpu_baseline = True   # the CPU leg compares CF32
     stream = torch.cuda.current_stream()
 
     if args.mode == "single":
         # weak scaling: rank r owns stream segment r (its own blocks + halo)
         d_in = make_input(torch, nblk, 0x5DDC + rank, dev)
-        d_out = torch.empty(output_samples(d, nblk) * 2, dtype=torch.float32, device=dev)
+        d_out = torch.empty(output_samples(d, nblk) * 2, dtype=out_dtype, device=dev)
         nch_local = 1
 
         def step():
             ddc.process_device(d_in, nblk, d_out, stream)
         samples_per_step_all = nblk * BLOCK * world
-        workload = f"single d={d} nblk={nblk}" + (f" fine_tune={args.fine_tune}" if args.fine_tune else "")
+        workload = f"single d={d} nblk={nblk}" + (f" fine_tune={args.fine_tune}" if args.fine_tune else "") \
+            + (" cs16" if args.cs16 else "")
     else:
         from extio_sddc_amd.shard import broadcast_samples, channel_shard
         tbs_all = [4 * c for c in range(args.channels)]
@@ -162,14 +171,14 @@ def main() -> None:
         d_in = make_input(torch, nblk, 0x5DDC, dev) if rank == 0 else \
             torch.empty(HALF + nblk * BLOCK, dtype=torch.int16, device=dev)
         per = output_samples(d, nblk) * 2
-        d_out = torch.empty((nch_local, per), dtype=torch.float32, device=dev)
+        d_out = torch.empty((nch_local, per), dtype=out_dtype, device=dev)
 
         def step():
             if world > 1:
                 broadcast_samples(d_in, src=0)
             ddc.process_channels_device(d_in, nblk, tbs, d_out, stream)
         samples_per_step_all = nblk * BLOCK          # one shared stream
-        workload = f"channels d={d} nblk={nblk} nch={args.channels}"
+        workload = f"channels d={d} nblk={nblk} nch={args.channels}" + (" cs16" if args.cs16 else "")
 
     for _ in range(args.warmup):
         step()
@@ -196,7 +205,7 @@ def main() -> None:
 
     value = samples_per_step_all * args.steps / wall / 1e6
     # roofline of the dominant kernel on THIS rank's launch
-    alg_bytes = nblk * BLOCK * algorithmic_bytes_per_sample(d, nch_local)
+    alg_bytes = nblk * BLOCK * algorithmic_bytes_per_sample(d, nch_local, out_bytes)
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     traffic = load_traffic(workload)
 
@@ -205,9 +214,9 @@ def main() -> None:
         "value": value, "unit": "input MSamples/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": wall * 1e3 / args.steps, "higher_is_better": True,
         "scaling": "weak" if args.mode == "single" else "strong",
-        "vs_baseline": None, "dtype": "f32 (int16 in, complex64 out)", "data": "synthetic",
+        "vs_baseline": None, "dtype": "f32 (int16 in, " + ("int16 IQ out)" if args.cs16 else "complex64 out)"), "data": "synthetic",
         "config": {"workload": "single-channel DDC, 128 MS/s int16 in, decim=2, 1xMI355X"
-                   if (args.mode == "single" and d == 0 and not args.fine_tune) else workload,
+                   if (args.mode == "single" and d == 0 and not args.fine_tune and not args.cs16) else workload,
                    "decim": 2 << d, "d": d, "tunebin": args.tunebin, "blocks_per_step_per_gpu": nblk,
                    "block_samples": BLOCK, "mode": args.mode,
                    "channels": args.channels if args.mode == "channels" else 1,
@@ -217,7 +226,7 @@ def main() -> None:
                      "kernel": "r2iq_persistent_kernel" if args.mode == "single" else "r2iq_channels_kernel",
                      "kernel_ms_per_launch": kern_ms,
                      "algorithmic_bytes_per_launch": alg_bytes,
-                     "bytes_per_input_sample": algorithmic_bytes_per_sample(d, nch_local)},
+                     "bytes_per_input_sample": algorithmic_bytes_per_sample(d, nch_local, out_bytes)},
     }
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
