@@ -15,3 +15,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/tra
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv --kernel-include-regex r2iq --pmc $c -d $O/pmc_$c -o run -- python3 $R/bench.py --no-cpu-baseline --steps 3 --warmup 1 > $O/pmc_$c.log 2>&1 || exit $?
 done
+# FETCH/WRITE calibration for the kernel's access widths (4 B/lane loads, 8 B/lane stores)
+for c in FETCH_SIZE WRITE_SIZE; do
+  timeout -k 10 120 rocprofv3 --kernel-trace --output-format csv --kernel-include-regex calib --pmc $c -d $O/calib_$c -o run -- $R/build/bin/pmc_calib > $O/calib_$c.log 2>&1 || exit $?
+done
