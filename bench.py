@@ -222,7 +222,10 @@ def main() -> None:
                    "channels": args.channels if args.mode == "channels" else 1,
                    "parallelism": f"time-segments x{world}" if args.mode == "single" else f"channels x{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": traffic["hbm_bytes_per_launch"] if traffic else None,
+                     "traffic_unit": "bytes per launch (rocprofv3 FETCH_SIZE/WRITE_SIZE, calibrated)",
+                     "traffic_detail": traffic,
                      "kernel": "r2iq_persistent_kernel" if args.mode == "single" else "r2iq_channels_kernel",
                      "kernel_ms_per_launch": kern_ms,
                      "algorithmic_bytes_per_launch": alg_bytes,
