@@ -48,6 +48,9 @@ constexpr bool kDB = SDDC_DB != 0;
 #ifndef SDDC_PQ
 #define SDDC_PQ 1             // split x filter from the per-(d, tunebin) coefficient table (P, Q)
 #endif
+#ifndef SDDC_PK
+#define SDDC_PK 0             // 1: radix-16 DFTs and twiddle products in packed FP32 (measured slower)
+#endif
 #ifndef SDDC_PREFETCH
 #define SDDC_PREFETCH 1       // load the next frame's input during the current one
 #endif
@@ -112,6 +115,52 @@ __device__ __forceinline__ void twiddle_rec16(float2 *a, float2 w1, float2 w4)
     a[13] = cmul(a[13], cmul(w12, w1));
     a[14] = cmul(a[14], cmul(w12, w2));
     a[15] = cmul(a[15], cmul(w12, w3));
+}
+
+// DFT-16 and twiddle products, packed (SDDC_PK) or scalar
+template <int DIR>
+__device__ __forceinline__ void DFT16(const float2 *a, float2 *v)
+{
+    if constexpr (SDDC_PK) pk::dft16<DIR>(a, v);
+    else dft16<DIR>(a, v);
+}
+// a * W (DIR < 0) or a * conj(W) (DIR > 0)
+template <int DIR>
+__device__ __forceinline__ float2 TW(float2 a, float2 w)
+{
+    if constexpr (SDDC_PK) return pk::F(DIR < 0 ? pk::cmul(pk::V(a), pk::V(w)) : pk::cmulc(pk::V(a), pk::V(w)));
+    else return DIR < 0 ? cmul(a, w) : cmulc(a, w);
+}
+// twiddle_rec16 with packed products
+template <int DIR>
+__device__ __forceinline__ void TWREC16(float2 *a, float2 w1_, float2 w4_)
+{
+    if constexpr (!SDDC_PK) {
+        twiddle_rec16<DIR>(a, w1_, w4_);
+        return;
+    }
+    using namespace pk;
+    f2v w1 = V(w1_), w4 = V(w4_);
+    if (DIR > 0) {
+        w1.y = -w1.y;
+        w4.y = -w4.y;
+    }
+    const f2v w2 = cmul(w1, w1), w3 = cmul(w2, w1), w8 = cmul(w4, w4), w12 = cmul(w8, w4);
+    a[1] = F(cmul(V(a[1]), w1));
+    a[2] = F(cmul(V(a[2]), w2));
+    a[3] = F(cmul(V(a[3]), w3));
+    a[4] = F(cmul(V(a[4]), w4));
+    a[5] = F(cmul(V(a[5]), cmul(w4, w1)));
+    a[6] = F(cmul(V(a[6]), cmul(w4, w2)));
+    a[7] = F(cmul(V(a[7]), cmul(w4, w3)));
+    a[8] = F(cmul(V(a[8]), w8));
+    a[9] = F(cmul(V(a[9]), cmul(w8, w1)));
+    a[10] = F(cmul(V(a[10]), cmul(w8, w2)));
+    a[11] = F(cmul(V(a[11]), cmul(w8, w3)));
+    a[12] = F(cmul(V(a[12]), w12));
+    a[13] = F(cmul(V(a[13]), cmul(w12, w1)));
+    a[14] = F(cmul(V(a[14]), cmul(w12, w2)));
+    a[15] = F(cmul(V(a[15]), cmul(w12, w3)));
 }
 
 // X[bin] * Hh[m] from Z in LDS (Hh = H/2): the r2c split E + W^bin O, times the filter.
@@ -238,7 +287,7 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
                 ++blk;
             }
             if (SDDC_PREFETCH && f + 1 < f1) load_frame(in32, blk, k, x);   // prefetch the next frame
-            dft16<-1>(a, v);
+            DFT16<-1>(a, v);
         }
         if constexpr (!kDB) LOOP_SYNC();   // the previous frame's last LDS reads are done
 #pragma unroll
@@ -251,8 +300,8 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
             for (int r = 0; r < 16; r++) a[r] = w0[sT + NT * r];
 #pragma unroll
             for (int r = 1; r < 16; r++)
-                a[r] = cmul(a[r], (SDDC_FAKE & 2) ? make_float2(0.7f, 0.01f * (r + x15)) : twl[(r - 1) * 16 + x15]);
-            dft16<-1>(a, v);
+                a[r] = TW<-1>(a[r], (SDDC_FAKE & 2) ? make_float2(0.7f, 0.01f * (r + x15)) : twl[(r - 1) * 16 + x15]);
+            DFT16<-1>(a, v);
         }
         if constexpr (!kDB) LOOP_SYNC();
         {
@@ -268,11 +317,11 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
             for (int r = 0; r < 16; r++) a[r] = w1[sT + NT * r];
             if constexpr (SDDC_TWTAB) {
 #pragma unroll
-                for (int r = 1; r < 16; r++) a[r] = cmul(a[r], ttf[(r - 1) * NT + t]);
+                for (int r = 1; r < 16; r++) a[r] = TW<-1>(a[r], ttf[(r - 1) * NT + t]);
             } else {
-                twiddle_rec16<-1>(a, fw1, fw4);
+                TWREC16<-1>(a, fw1, fw4);
             }
-            dft16<-1>(a, v);
+            DFT16<-1>(a, v);
         }
         if constexpr (!kDB) LOOP_SYNC();
 #pragma unroll
@@ -324,7 +373,8 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
                         a[r] = ok ? val : make_float2(0.f, 0.f);
                     }
                 }
-                dft<R0, +1>(a, u);
+                if constexpr (R0 == 16) DFT16<+1>(a, u);
+                else dft<R0, +1>(a, u);
             }
             if constexpr (!kDB) LOOP_SYNC();
             if constexpr (R0 == 16) {
@@ -349,8 +399,8 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
                 }
 #pragma unroll
                 for (int r = 1; r < 16; r++)
-                    a[r] = cmulc(a[r], (SDDC_FAKE & 2) ? make_float2(0.7f, 0.01f * (r + t % R0)) : twl[15 * 16 + (r - 1) * R0 + (t % R0)]);
-                dft16<+1>(a, u);
+                    a[r] = TW<+1>(a[r], (SDDC_FAKE & 2) ? make_float2(0.7f, 0.01f * (r + t % R0)) : twl[15 * 16 + (r - 1) * R0 + (t % R0)]);
+                DFT16<+1>(a, u);
             }
             if constexpr (!kDB) LOOP_SYNC();
             if (act) {
@@ -377,11 +427,11 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
                 }
                 if constexpr (SDDC_TWTAB) {
 #pragma unroll
-                    for (int r = 1; r < 16; r++) a[r] = cmulc(a[r], (N == HALF ? ttf : tti)[(r - 1) * NB + t]);
+                    for (int r = 1; r < 16; r++) a[r] = TW<+1>(a[r], (N == HALF ? ttf : tti)[(r - 1) * NB + t]);
                 } else {
-                    twiddle_rec16<+1>(a, iw1, iw4);
+                    TWREC16<+1>(a, iw1, iw4);
                 }
-                dft16<+1>(a, u);
+                DFT16<+1>(a, u);
                 emit_frame<NB, NCO, CS16>(out, oblk + emit_base<N>(kc), kc, t, u, oa, nco);
             }
         } else {
@@ -418,8 +468,8 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
 #pragma unroll
                 for (int r = 0; r < 16; r++) a[r] = w0[swz(t + NB * r)];
 #pragma unroll
-                for (int r = 1; r < 16; r++) a[r] = cmulc(a[r], twl[15 * 16 + (r - 1) * NB + t]);
-                dft16<+1>(a, u);
+                for (int r = 1; r < 16; r++) a[r] = TW<+1>(a[r], twl[15 * 16 + (r - 1) * NB + t]);
+                DFT16<+1>(a, u);
                 emit_frame<NB, NCO, CS16>(out, oblk + emit_base<N>(kc), kc, t, u, oa, nco);
             }
         }

@@ -141,6 +141,106 @@ __device__ __forceinline__ void dft(const float2 *v, float2 *o)
 }
 
 // ---------------------------------------------------------------------------
+// Packed-FP32 variants (gfx950 v_pk_{add,mul,fma}_f32 on (re, im) register pairs).
+// The ±i rotations and the operand swaps of a complex product ride on the VOP3P
+// op_sel / op_sel_hi / neg_lo / neg_hi source modifiers, so a butterfly is one
+// instruction, a twiddle multiply two, and a radix-16 DFT 80 (vs ~154 scalar).
+// ---------------------------------------------------------------------------
+namespace pk {
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f2v V(float2 a) { return f2v{a.x, a.y}; }
+__device__ __forceinline__ float2 F(f2v a) { return make_float2(a.x, a.y); }
+
+// t + DIR*i*d  and  t - DIR*i*d  (mulj<DIR>, one instruction each)
+template <int DIR>
+__device__ __forceinline__ f2v addj(f2v t, f2v d)
+{
+    f2v r;
+    if constexpr (DIR < 0)   // (t.x + d.y, t.y - d.x)
+        asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(t), "v"(d));
+    else                     // (t.x - d.y, t.y + d.x)
+        asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(t), "v"(d));
+    return r;
+}
+template <int DIR>
+__device__ __forceinline__ f2v subj(f2v t, f2v d)
+{
+    return addj<-DIR>(t, d);
+}
+
+// a * w and a * conj(w): t = (a.x w.x, a.y w.x); r = t + (a.y, a.x) * (-+w.y, +-w.y)
+__device__ __forceinline__ f2v cmul(f2v a, f2v w)
+{
+    f2v t, r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(t) : "v"(a), "v"(w));
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_lo:[0,1,0]"
+        : "=v"(r) : "v"(a), "v"(w), "v"(t));
+    return r;
+}
+__device__ __forceinline__ f2v cmulc(f2v a, f2v w)
+{
+    f2v t, r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(t) : "v"(a), "v"(w));
+    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_hi:[0,1,0]"
+        : "=v"(r) : "v"(a), "v"(w), "v"(t));
+    return r;
+}
+
+// e^{DIR*2*pi*i*m/16} as (cos, sin) constants
+template <int DIR, int M>
+__device__ __forceinline__ f2v w16()
+{
+    constexpr int m = M & 15;
+    constexpr float c = (m == 1 || m == 15) ? kC16_1 : (m == 3 || m == 13) ? kS16_1
+                      : (m == 5 || m == 11) ? -kS16_1 : (m == 7 || m == 9) ? -kC16_1
+                      : (m == 2 || m == 14) ? kR2 : (m == 6 || m == 10) ? -kR2 : 0.f;
+    constexpr float s = (m == 1 || m == 7) ? kS16_1 : (m == 3 || m == 5) ? kC16_1
+                      : (m == 9 || m == 15) ? -kS16_1 : (m == 11 || m == 13) ? -kC16_1
+                      : (m == 2 || m == 6) ? kR2 : (m == 10 || m == 14) ? -kR2 : 0.f;
+    return f2v{c, DIR * s};
+}
+
+// natural order in -> natural order out; a2 is multiplied by DIR*i first when J2
+template <int DIR, bool J2 = false>
+__device__ __forceinline__ void dft4(f2v a0, f2v a1, f2v a2, f2v a3, f2v &o0, f2v &o1, f2v &o2, f2v &o3)
+{
+    const f2v t0 = J2 ? addj<DIR>(a0, a2) : a0 + a2;
+    const f2v t1 = J2 ? subj<DIR>(a0, a2) : a0 - a2;
+    const f2v t2 = a1 + a3, d = a1 - a3;
+    o0 = t0 + t2;
+    o2 = t0 - t2;
+    o1 = addj<DIR>(t1, d);
+    o3 = subj<DIR>(t1, d);
+}
+
+// 16 = 4 x 4 as sddc::dft16, with W_16^4 folded into the second stage
+template <int DIR>
+__device__ __forceinline__ void dft16(const float2 *v, float2 *o)
+{
+    f2v b[4][4];
+#pragma unroll
+    for (int n2 = 0; n2 < 4; n2++)
+        dft4<DIR>(V(v[n2]), V(v[4 + n2]), V(v[8 + n2]), V(v[12 + n2]), b[n2][0], b[n2][1], b[n2][2], b[n2][3]);
+    b[1][1] = cmul(b[1][1], w16<DIR, 1>());
+    b[1][2] = cmul(b[1][2], w16<DIR, 2>());
+    b[1][3] = cmul(b[1][3], w16<DIR, 3>());
+    b[2][1] = cmul(b[2][1], w16<DIR, 2>());
+    b[2][3] = cmul(b[2][3], w16<DIR, 6>());
+    b[3][1] = cmul(b[3][1], w16<DIR, 3>());
+    b[3][2] = cmul(b[3][2], w16<DIR, 6>());
+    b[3][3] = cmul(b[3][3], w16<DIR, 9>());
+    f2v r[16];
+    dft4<DIR>(b[0][0], b[1][0], b[2][0], b[3][0], r[0], r[4], r[8], r[12]);
+    dft4<DIR>(b[0][1], b[1][1], b[2][1], b[3][1], r[1], r[5], r[9], r[13]);
+    dft4<DIR, true>(b[0][2], b[1][2], b[2][2], b[3][2], r[2], r[6], r[10], r[14]);   // b[2][2] * W^4
+    dft4<DIR>(b[0][3], b[1][3], b[2][3], b[3][3], r[3], r[7], r[11], r[15]);
+#pragma unroll
+    for (int k = 0; k < 16; k++) o[k] = F(r[k]);
+}
+}  // namespace pk
+
+// ---------------------------------------------------------------------------
 // LDS layout: complex element i lives at float2 slot lds_pad(i) = i + i/16.
 // One pad slot per 16 elements keeps the radix-16 "16 consecutive per lane"
 // writes of the first pass conflict-free on ds_write_b64 (bank = dword/2 mod 32).
