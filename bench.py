@@ -89,6 +89,44 @@ def cpu_baseline(d: int, tunebin: int, gpu_sample_out, sample_in: np.ndarray, nb
     }
 
 
+_CPU_WORKER = r"""
+import sys, time, numpy as np
+sys.path.insert(0, sys.argv[1])
+from oracle import oracle as O
+x = np.load(sys.argv[2]); nblk, d, tb, budget = int(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5]), float(sys.argv[6])
+H = O.filter_bank(1.0, np.float32)
+O.r2iq(x, 1, d, tb, dtype=np.float32, H=H)
+done, t0 = 0, time.perf_counter()
+while time.perf_counter() - t0 < budget:
+    O.r2iq(x, nblk, d, tb, dtype=np.float32, H=H); done += nblk
+print(done, time.perf_counter() - t0)
+"""
+
+
+def cpu_baseline_all_cores(d: int, tunebin: int, sample_in: np.ndarray, nblk_sample: int, budget_s: float) -> dict:
+    """one independent f32-port instance per core of this process's CPU
+    share (at most 16, the GPU box's share), as child processes that never touch the GPU."""
+    import tempfile
+    try:
+        ncores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        ncores = os.cpu_count() or 1
+    procs = max(1, min(16, ncores))
+    with tempfile.TemporaryDirectory(dir="/tmp") as td:
+        path = os.path.join(td, "sample.npy")
+        np.save(path, sample_in)
+        env = dict(os.environ, OMP_NUM_THREADS="1")
+        ps = [subprocess.Popen([sys.executable, "-c", _CPU_WORKER, ROOT, path, str(nblk_sample), str(d), str(tunebin),
+                                str(budget_s)], stdout=subprocess.PIPE, text=True, env=env) for _ in range(procs)]
+        total = 0.0
+        for p in ps:
+            out, _ = p.communicate(timeout=budget_s * 4 + 60)
+            done, dt = out.split()
+            total += int(done) * BLOCK / float(dt)
+    return {"value": total / 1e6, "unit": "input MSamples/s", "cores": procs, "kind": "port",
+            "sample": f"{procs} independent processes x the 1-core sample, {budget_s:.1f} s each"}
+
+
 def load_traffic(workload: str):
     """Per-launch HBM bytes measured with rocprofv3 --pmc (profiles/pmc_traffic.json), if present."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -243,6 +281,10 @@ def main() -> None:
             tb = tbs[0]
         # d_out holds the whole batch; its first ns blocks depend only on the first ns blocks
         cb = cpu_baseline(d, tb, gout, sample, ns, args.cpu_budget)
+        try:
+            cb["all_cores"] = cpu_baseline_all_cores(d, tb, sample, ns, args.cpu_budget)
+        except Exception as e:   # the 1-core figure stands on its own
+            cb["all_cores"] = {"error": str(e)}
         result["cpu_baseline"] = cb
         result["iq_max_rel_err"] = cb.pop("iq_max_rel_err_gpu_vs_oracle_f64")
         result["iq_rms_rel_err"] = cb.pop("iq_rms_rel_err_gpu_vs_oracle_f64")
