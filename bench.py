@@ -127,6 +127,18 @@ def cpu_baseline_all_cores(d: int, tunebin: int, sample_in: np.ndarray, nblk_sam
             "sample": f"{procs} independent processes x the 1-core sample, {budget_s:.1f} s each"}
 
 
+def reference_equivalent(port_msps: float, d: int):
+    """Scale an on-box port timing by the committed port-vs-reference ratio
+    (profiles/cpu_calibration.json, tools/cpu_calib.py): an estimate, labelled as such."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "cpu_calibration.json")) as f:
+            r = json.load(f)["ratio_reference_over_port"][str(d)]
+        return {"value": port_msps * r, "ratio": r,
+                "basis": "reference AVX2 r2iq / f32 port, both 1 core of the survey container (BASELINE.md §2)"}
+    except Exception:
+        return None
+
+
 def load_traffic(workload: str):
     """Per-launch HBM bytes measured with rocprofv3 --pmc (profiles/pmc_traffic.json), if present."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -151,6 +163,8 @@ def main() -> None:
     ap.add_argument("--channels", type=int, default=1024)
     ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds of CPU-baseline work")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-sweep", action="store_true",
+                    help="skip the same-run C3 decim sweep / C4 VHF lines (BASELINE.md §3)")
     ap.add_argument("--cs16", type=float, default=0.0,
                     help="CS16 output with this scale (int16 = rint(x * scale)); 0 = CF32")
     ap.add_argument("--fine-tune", type=float, default=0.0,
@@ -285,9 +299,46 @@ def main() -> None:
             cb["all_cores"] = cpu_baseline_all_cores(d, tb, sample, ns, args.cpu_budget)
         except Exception as e:   # the 1-core figure stands on its own
             cb["all_cores"] = {"error": str(e)}
+        cb["reference_equivalent_estimate"] = reference_equivalent(cb["value"], d)
         result["cpu_baseline"] = cb
         result["iq_max_rel_err"] = cb.pop("iq_max_rel_err_gpu_vs_oracle_f64")
         result["iq_rms_rel_err"] = cb.pop("iq_rms_rel_err_gpu_vs_oracle_f64")
+    if rank == 0 and world == 1 and args.mode == "single" and not args.no_sweep and not (args.cs16 or args.fine_tune):
+        # BASELINE.md §3 / SURVEY §8(d) C3 + C4, same run: GPU rate and roofline per config (the
+        # headline value above stays the d=0 line); CPU port 1 core on the same 16-block sample
+        lines = []
+        for dd, lsb, rnd, name in [(0, 0, 0, "C3 decim 2"), (1, 0, 0, "C3 decim 4"), (2, 0, 0, "C3 decim 8"),
+                                   (3, 0, 0, "C3 decim 16"), (4, 0, 0, "C3 decim 32"),
+                                   (1, 1, 1, "C4 VHF decim 4, sideband invert, rand")]:
+            ddc.setDecimate(dd)
+            ddc.setSideband(bool(lsb))
+            ddc.updateRand(bool(rnd))
+            for _ in range(10):
+                ddc.process_device(d_in, nblk, d_out, stream)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()
+            e0.record(stream)
+            for _ in range(30):
+                ddc.process_device(d_in, nblk, d_out, stream)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / 30
+            line = {"config": name, "d": dd, "lsb": lsb, "rand": rnd, "gpu_input_MSps": nblk * BLOCK / ms / 1e3,
+                    "roofline_frac": nblk * BLOCK * algorithmic_bytes_per_sample(dd) / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                    "kernel_ms": ms}
+            if not args.no_cpu_baseline:
+                ns = 16
+                sample = d_in[: HALF + ns * BLOCK].cpu().numpy()
+                gout = d_out[: output_samples(dd, ns) * 2].cpu().numpy().view(np.complex64)
+                if rnd or lsb:
+                    line["cpu_port_1core_MSps"] = None   # the CPU leg times the plain path only
+                else:
+                    cbd = cpu_baseline(dd, args.tunebin, gout, sample, ns, 2.0)
+                    line["cpu_port_1core_MSps"] = cbd["value"]
+                    line["cpu_reference_equivalent_MSps"] = (reference_equivalent(cbd["value"], dd) or {}).get("value")
+                    line["iq_max_rel_err"] = cbd["iq_max_rel_err_gpu_vs_oracle_f64"]
+            lines.append(line)
+        result["sweep"] = lines
     if rank == 0:
         result["host"] = platform.node()
         print(json.dumps(result), flush=True)
