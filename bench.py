@@ -255,6 +255,34 @@ def main() -> None:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall, kern_ms = t.tolist()
 
+    # BASELINE.md §3 / SURVEY §8(d) C3 + C4 in the same run, while the clocks are at their
+    # steady state: GPU rate and roofline per config (the headline value stays the d=0 line)
+    sweep = []
+    if rank == 0 and world == 1 and args.mode == "single" and not args.no_sweep and not (args.cs16 or args.fine_tune):
+        for dd, lsb, rnd, name in [(0, 0, 0, "C3 decim 2"), (1, 0, 0, "C3 decim 4"), (2, 0, 0, "C3 decim 8"),
+                                   (3, 0, 0, "C3 decim 16"), (4, 0, 0, "C3 decim 32"),
+                                   (1, 1, 1, "C4 VHF decim 4, sideband invert, rand")]:
+            ddc.setDecimate(dd)
+            ddc.setSideband(bool(lsb))
+            ddc.updateRand(bool(rnd))
+            for _ in range(30):
+                ddc.process_device(d_in, nblk, d_out, stream)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(50):
+                ddc.process_device(d_in, nblk, d_out, stream)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / 50
+            sweep.append({"config": name, "d": dd, "lsb": lsb, "rand": rnd, "gpu_input_MSps": nblk * BLOCK / ms / 1e3,
+                          "roofline_frac": nblk * BLOCK * algorithmic_bytes_per_sample(dd) / (ms * 1e-3) / 1e9
+                          / HBM_PEAK_GBS, "kernel_ms": ms})
+        ddc.setDecimate(d)
+        ddc.setSideband(False)
+        ddc.updateRand(False)
+        ddc.process_device(d_in, nblk, d_out, stream)   # d_out holds the headline config again
+        torch.cuda.synchronize()
+
     value = samples_per_step_all * args.steps / wall / 1e6
     # roofline of the dominant kernel on THIS rank's launch
     alg_bytes = nblk * BLOCK * algorithmic_bytes_per_sample(d, nch_local, out_bytes)
@@ -303,42 +331,19 @@ def main() -> None:
         result["cpu_baseline"] = cb
         result["iq_max_rel_err"] = cb.pop("iq_max_rel_err_gpu_vs_oracle_f64")
         result["iq_rms_rel_err"] = cb.pop("iq_rms_rel_err_gpu_vs_oracle_f64")
-    if rank == 0 and world == 1 and args.mode == "single" and not args.no_sweep and not (args.cs16 or args.fine_tune):
-        # BASELINE.md §3 / SURVEY §8(d) C3 + C4, same run: GPU rate and roofline per config (the
-        # headline value above stays the d=0 line); CPU port 1 core on the same 16-block sample
-        lines = []
-        for dd, lsb, rnd, name in [(0, 0, 0, "C3 decim 2"), (1, 0, 0, "C3 decim 4"), (2, 0, 0, "C3 decim 8"),
-                                   (3, 0, 0, "C3 decim 16"), (4, 0, 0, "C3 decim 32"),
-                                   (1, 1, 1, "C4 VHF decim 4, sideband invert, rand")]:
-            ddc.setDecimate(dd)
-            ddc.setSideband(bool(lsb))
-            ddc.updateRand(bool(rnd))
-            for _ in range(10):
-                ddc.process_device(d_in, nblk, d_out, stream)
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            torch.cuda.synchronize()
-            e0.record(stream)
-            for _ in range(30):
-                ddc.process_device(d_in, nblk, d_out, stream)
-            e1.record(stream)
-            torch.cuda.synchronize()
-            ms = e0.elapsed_time(e1) / 30
-            line = {"config": name, "d": dd, "lsb": lsb, "rand": rnd, "gpu_input_MSps": nblk * BLOCK / ms / 1e3,
-                    "roofline_frac": nblk * BLOCK * algorithmic_bytes_per_sample(dd) / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                    "kernel_ms": ms}
-            if not args.no_cpu_baseline:
-                ns = 16
-                sample = d_in[: HALF + ns * BLOCK].cpu().numpy()
+    if sweep:
+        for line in sweep:
+            if not args.no_cpu_baseline and not (line["lsb"] or line["rand"]):
+                dd, ns = line["d"], 16
+                ddc.setDecimate(dd)
+                ddc.process_device(d_in, ns, d_out, stream)
+                torch.cuda.synchronize()
                 gout = d_out[: output_samples(dd, ns) * 2].cpu().numpy().view(np.complex64)
-                if rnd or lsb:
-                    line["cpu_port_1core_MSps"] = None   # the CPU leg times the plain path only
-                else:
-                    cbd = cpu_baseline(dd, args.tunebin, gout, sample, ns, 2.0)
-                    line["cpu_port_1core_MSps"] = cbd["value"]
-                    line["cpu_reference_equivalent_MSps"] = (reference_equivalent(cbd["value"], dd) or {}).get("value")
-                    line["iq_max_rel_err"] = cbd["iq_max_rel_err_gpu_vs_oracle_f64"]
-            lines.append(line)
-        result["sweep"] = lines
+                cbd = cpu_baseline(dd, args.tunebin, gout, d_in[: HALF + ns * BLOCK].cpu().numpy(), ns, 2.0)
+                line["cpu_port_1core_MSps"] = cbd["value"]
+                line["cpu_reference_equivalent_MSps"] = (reference_equivalent(cbd["value"], dd) or {}).get("value")
+                line["iq_max_rel_err"] = cbd["iq_max_rel_err_gpu_vs_oracle_f64"]
+        result["sweep"] = sweep
     if rank == 0:
         result["host"] = platform.node()
         print(json.dumps(result), flush=True)
