@@ -459,7 +459,8 @@ int sddc_ddc_internal_set_variant(sddc_ddc_t *h, int variant)
 static int check_process_args(sddc_ddc_t *h, const int16_t *in, int nblk, const void *out)
 {
     if (!h) return fail(SDDC_ERR_ARG, "null handle");
-    if (nblk <= 0) return fail(SDDC_ERR_ARG, "nblk must be > 0 (got %d)", nblk);
+    if (nblk <= 0 || nblk > SDDC_DDC_MAX_BLOCKS)
+        return fail(SDDC_ERR_ARG, "nblk must be in 1..%d (got %d)", SDDC_DDC_MAX_BLOCKS, nblk);
     if (!in || !out) return fail(SDDC_ERR_ARG, "null buffer");
     if (((uintptr_t)in & 3) != 0) return fail(SDDC_ERR_ARG, "input must be 4-byte aligned");
     const unsigned oal = h->out_fmt == SDDC_DDC_FMT_CS16 ? 4 : 8;

@@ -45,6 +45,7 @@ extern "C" {
 #define SDDC_DDC_NTAPS      1025    /* halfFft/4+1 taps      fft_mt_r2iq.cpp:181 */
 #define SDDC_DDC_OUT_BLOCK  32768   /* EXT_BLOCKLEN          config.h:62 */
 #define SDDC_DDC_MAX_CHANNELS 1024  /* 1024 legal tune bins (tunebin = 4c) */
+#define SDDC_DDC_MAX_BLOCKS 32768   /* blocks per process_* call (2^31 input samples, 4 GiB) */
 
 enum {
     SDDC_OK = 0,

@@ -228,3 +228,18 @@ def test_bad_arguments_raise(torch_dev, ddc):
         ddc.setTuneBin(4096)
     with pytest.raises(DDCError):
         ddc.process(np.zeros(1000, np.int16))
+
+
+def test_block_limit_and_empty_calls(torch_dev, ddc):
+    """nblk outside 1..SDDC_DDC_MAX_BLOCKS is refused before any device work (32-bit output
+    indexing in the kernels); an empty host call is refused too."""
+    from extio_sddc_amd import DDCError
+    from extio_sddc_amd._lib import check
+    torch = torch_dev
+    x = torch.zeros(4096 + 65536, dtype=torch.int16, device="cuda")
+    y = torch.zeros(2 * 32768, dtype=torch.float32, device="cuda")
+    for bad in (0, -1, 32769):
+        with pytest.raises(DDCError):
+            check(ddc._L.sddc_ddc_process_device(ddc._h, x.data_ptr(), bad, y.data_ptr(), None))
+    with pytest.raises(DDCError):
+        ddc.process(np.zeros(0, np.int16))
