@@ -65,3 +65,27 @@ def test_reference_radiohandler_runs_dropin(tmp_path, oracle, srate_idx, tune_hz
     ref = oracle.r2iq(x, nblk, d, tb, False, rand, gain=float(BBRF103_GAINFACTOR))
     assert y.size == ref.size                # every callback carries 32768 samples (core_test.cpp:167)
     assert oracle.max_rel_err(y, ref) <= TOL
+
+
+@pytest.mark.skipif(not os.path.exists(RH_HARNESS), reason="reference RadioHandler harness not built here")
+@pytest.mark.parametrize("srate_idx,tune_hz,rand", [(4, 7_777_777, 0), (2, 5_003_000, 1)])
+def test_reference_radiohandler_fine_tune(tmp_path, oracle, srate_idx, tune_hz, rand):
+    """A tune between 4-bin steps: RadioHandler::TuneLO gets a non-zero residual fc from our
+    setFreqOffset and its own CPU mixer (pf_mixer ALGO H, RadioHandler.cpp:33-37) runs on our
+    output.  Expected: oracle DDC at tb, then the oracle mixer (bit-exact to pf_mixer)."""
+    d = 4 - srate_idx
+    nblk = max(4, 2 << d)
+    x = make_stream(nblk, "mix")
+    fin, fout = tmp_path / "in.bin", tmp_path / "out.bin"
+    x[4096:].tofile(fin)
+    _run([RH_HARNESS, str(fin), str(nblk), str(srate_idx), str(tune_hz), str(rand), str(fout)])
+    y = np.fromfile(fout, np.float32).view(np.complex64)
+    # RadioHandler.cpp:289: offset / (getSampleRate() / 2.0f), all in float.  The harness tunes
+    # before Start() sets the decimation, so setFreqOffset scales the residual by getRatio() of
+    # d = 0 (r2iq.h:24, mratio[0] = 1): the reference's behaviour for this call order.
+    tb, fc = oracle.set_freq_offset(np.float32(np.float32(tune_hz) / np.float32(32e6)), 0)
+    assert fc != 0.0
+    plain = oracle.r2iq(x, nblk, d, tb, False, rand, gain=float(BBRF103_GAINFACTOR)).astype(np.complex64)
+    ref = oracle.Nco(fc).apply(plain)
+    assert y.size == ref.size
+    assert oracle.max_rel_err(y, ref) <= TOL
