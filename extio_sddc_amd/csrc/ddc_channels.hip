@@ -30,6 +30,24 @@ constexpr int CHUNK = 128;    // channels per work item
 
 __device__ __forceinline__ int swz(int e) { return e ^ ((e >> 4) & 15); }
 
+#ifndef SDDC_CH_WAVESYNC
+#define SDDC_CH_WAVESYNC 1   // the per-channel exchange is wave-local: order it within the wave only
+#endif
+
+// A channel's TPC threads are consecutive lanes of one wave and only they touch its slice of
+// `work`, so the pass A -> pass B exchange (and the WAR before the next group) needs program
+// order within the wave, not a workgroup barrier.  LDS operations of a wave execute in order.
+__device__ __forceinline__ void channel_sync()
+{
+    if constexpr (SDDC_CH_WAVESYNC) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    } else {
+        __syncthreads();
+    }
+}
+
 template <bool RAND>
 __device__ __forceinline__ float derand(int v)
 {
@@ -184,7 +202,7 @@ __global__ __launch_bounds__(NT, 2) void r2iq_channels_v2_kernel(
 #pragma unroll
                 for (int r = 0; r < 16; r++) wg[swz(16 * l + r)] = u[r];
             }
-            __syncthreads();
+            channel_sync();
             // pass B: radix-RB Stockham step (NS = 16), twiddles W_N^{j q} = W_256^{(256/N) j q}
             if (cok) {
                 char *ob = static_cast<char *>(out) + ((size_t)c * stride + (size_t)blk * 8 * N) * out_bytes<CS16>();
@@ -217,7 +235,7 @@ __global__ __launch_bounds__(NT, 2) void r2iq_channels_v2_kernel(
                     }
                 }
             }
-            __syncthreads();   // wg is rewritten by the next channel group
+            channel_sync();   // wg is rewritten by the next channel group (same lanes)
         }
     }
 }

@@ -10,6 +10,8 @@ from __future__ import annotations
 import argparse
 import ctypes
 import json
+
+import numpy as np
 import os
 import sys
 
@@ -25,6 +27,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=10)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--tunebin", type=int, default=1024)
+    ap.add_argument("--channels", type=int, default=0, help="time process_channels_device with tune bins 4c")
     args = ap.parse_args()
 
     import torch
@@ -57,7 +60,9 @@ def main():
     del heat
     for d in args.d:
         n_out = nblk * (32768 >> d) * 2
-        outs = [torch.empty(n_out, dtype=torch.float32, device=dev) for _ in libs]
+        nch = max(args.channels, 1)
+        outs = [torch.empty(n_out * nch, dtype=torch.float32, device=dev) for _ in libs]
+        tbs = np.ascontiguousarray(np.arange(nch, dtype=np.int32) * 4)
         times = [[] for _ in libs]
         for L, h in zip(libs, handles):
             L.sddc_ddc_set_decimation(h, d)
@@ -66,7 +71,11 @@ def main():
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 for _ in range(args.reps):
-                    rc = L.sddc_ddc_process_device(h, d_in.data_ptr(), nblk, outs[i].data_ptr(), s)
+                    if args.channels:
+                        rc = L.sddc_ddc_process_channels_device(h, d_in.data_ptr(), nblk, tbs.ctypes.data, nch,
+                                                                outs[i].data_ptr(), n_out, s)
+                    else:
+                        rc = L.sddc_ddc_process_device(h, d_in.data_ptr(), nblk, outs[i].data_ptr(), s)
                     assert rc == 0, L.sddc_ddc_last_error()
                 e1.record()
                 torch.cuda.synchronize()
@@ -77,7 +86,7 @@ def main():
             med = ts[len(ts) // 2]
             diff = ((outs[i] - outs[0]).abs().max() / outs[0].abs().max()).item()
             gs = nblk * 65536 / (med * 1e-3) / 1e9
-            frac = nblk * 65536 * (2 + 4 / (1 << d)) / (med * 1e-3) / 8e12
+            frac = nblk * 65536 * (2 + 4 * nch / (1 << d)) / (med * 1e-3) / 8e12
             res[f"d{d}:{os.path.basename(p)}"] = {"median_ms": med, "min_ms": ts[0], "GSps": gs, "hbm_frac": frac,
                                                   "maxrel_vs_first": diff}
             print(f"d={d} {os.path.basename(p):28s} median {med:.3f} ms min {ts[0]:.3f}  {gs:7.1f} GS/s  "
