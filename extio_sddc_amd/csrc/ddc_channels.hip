@@ -13,6 +13,8 @@
 // CUs x resident workgroups, contiguous item ranges.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "ddc_consts.h"
 #include "ddc_kernels.h"
 #include "fft_device.hpp"
@@ -27,6 +29,7 @@ constexpr int HOP = 6144;
 constexpr int BLOCK = 65536;
 constexpr int FRAMES = 11;
 constexpr int CHUNK = 128;    // channels per work item
+constexpr int ZC_MAX = 1536;  // compact window of forward bins per chunk (window + its mirror)
 
 __device__ __forceinline__ int swz(int e) { return e ^ ((e >> 4) & 15); }
 
@@ -90,12 +93,15 @@ __device__ __forceinline__ constexpr float2 wsplit(int r)
     else return make_float2(kWsplitRe64[r], kWsplitIm64[r]);
 }
 
-template <int D, bool RAND, bool CS16>
+// COMPACT: after the forward transform the chunk's bins [lo, lo + w) and their mirrors are
+// copied into a window zcw (host-checked to fit ZC_MAX), and the per-channel slices reuse the
+// transform buffer: 48 KB of LDS instead of 68 KB, three workgroups per CU instead of two.
+template <int D, bool RAND, bool CS16, bool COMPACT>
 __global__ __launch_bounds__(NT, 2) void r2iq_channels_v2_kernel(
     const int *__restrict__ in32, void *__restrict__ out, size_t stride, int nframes,
     const int *__restrict__ tunebins, int nch, const float2 *__restrict__ tw_p1,
     const float2 *__restrict__ rec_f, const float2 *__restrict__ post8192, const float2 *__restrict__ hsel,
-    OutArgs oa)
+    OutArgs oa, const int2 *__restrict__ windows)
 {
     constexpr int N = HALF >> D;
     static_assert(N <= 256 && N >= 64, "channels v2 covers d = 4..6");
@@ -104,8 +110,11 @@ __global__ __launch_bounds__(NT, 2) void r2iq_channels_v2_kernel(
     constexpr int RB = N / 16;           // pass-B radix
     constexpr int BPT = 16 / TPC;        // pass-B butterflies per thread
 
-    __shared__ __attribute__((aligned(16))) float2 zl[HALF];
-    __shared__ __attribute__((aligned(16))) float2 work[G * N];
+    static_assert(G * N == HALF, "per-channel slices fill exactly one transform buffer");
+    __shared__ __attribute__((aligned(16))) float2 zbuf[COMPACT ? HALF + ZC_MAX : 2 * HALF];
+    float2 *const zl = zbuf;                              // forward transform
+    float2 *const work = COMPACT ? zbuf : zbuf + HALF;    // channel slices (reuse zl when COMPACT)
+    float2 *const zcw = zbuf + HALF;                      // COMPACT: [window | mirror window]
     __shared__ __attribute__((aligned(16))) float2 twl[15 * 16];
     __shared__ __attribute__((aligned(16))) float2 hl[N];
 
@@ -170,6 +179,20 @@ __global__ __launch_bounds__(NT, 2) void r2iq_channels_v2_kernel(
 #pragma unroll
         for (int r = 0; r < 16; r++) zl[sT + NT * r] = v[r];
         __syncthreads();
+        int lo = 0, lo2 = 0, w1 = 0;
+        if constexpr (COMPACT) {
+            // bins [lo, lo + w1) of this chunk's channels, then their mirrors (4096 - b) & 4095,
+            // which run contiguously (mod 4096) from lo2 = (4097 - lo - w1) & 4095
+            const int2 wv = windows[chunk];
+            lo = wv.x;
+            w1 = wv.y;
+            lo2 = (HALF + 1 - lo - w1) & (HALF - 1);
+            for (int i = t; i < 2 * w1; i += NT) {
+                const int bin = i < w1 ? lo + i : (lo2 + i - w1) & (HALF - 1);
+                zcw[i] = zl[swz(bin)];
+            }
+            __syncthreads();   // zl is overwritten by the channel slices from here on
+        }
 
         // ---------------- channels, G at a time ----------------
         const int cbeg = chunk * CHUNK;
@@ -189,8 +212,17 @@ __global__ __launch_bounds__(NT, 2) void r2iq_channels_v2_kernel(
                     const bool wrap = TPC * r >= N / 2;
                     const int bin = tb + m - (wrap ? N : 0);
                     const bool ok = cok && (unsigned)bin < (unsigned)HALF;
-                    const float2 zk = zl[swz(bin & (HALF - 1))];
-                    const float2 zc = zl[swz((HALF - bin) & (HALF - 1))];
+                    float2 zk, zc;
+                    if constexpr (COMPACT) {
+                        // out-of-window bins only occur for !ok legs (masked below); clamp the index
+                        const int i1 = min(max(bin - lo, 0), w1 - 1);
+                        const int i2 = min(max(((HALF - bin) - lo2) & (HALF - 1), 0), w1 - 1);
+                        zk = zcw[i1];
+                        zc = zcw[w1 + i2];
+                    } else {
+                        zk = zl[swz(bin & (HALF - 1))];
+                        zc = zl[swz((HALF - bin) & (HALF - 1))];
+                    }
                     const float2 A = make_float2(zk.x + zc.x, zk.y - zc.y);
                     const float2 Bi = make_float2(zk.y + zc.y, zc.x - zk.x);   // (Zk - conj Zc)/i
                     const float2 wb = cmul(pbc, wsplit<N>(r));
@@ -240,53 +272,85 @@ __global__ __launch_bounds__(NT, 2) void r2iq_channels_v2_kernel(
     }
 }
 
-int g_occ[3][4] = {};
+int g_occ[3][8] = {};
 int g_cus = 0;
 
-template <int D, bool RAND, bool CS16>
-hipError_t launch_v(const KernelTables &t, const int16_t *d_in, int nblk, const int *d_tunebins, int nch,
-                    void *d_out, size_t stride, OutArgs oa, int device, hipStream_t s)
+struct ChLaunch {
+    const int16_t *d_in;
+    int nblk;
+    const int *d_tunebins;
+    int nch;
+    void *d_out;
+    size_t stride;
+    OutArgs oa;
+    const int2 *windows;   // per-chunk compact windows, or nullptr
+    int device;
+    hipStream_t s;
+};
+
+template <int D, bool RAND, bool CS16, bool COMPACT>
+hipError_t launch_v(const KernelTables &t, const ChLaunch &L)
 {
-    auto kern = r2iq_channels_v2_kernel<D, RAND, CS16>;
-    int &occ = g_occ[D - 4][(RAND ? 2 : 0) + (CS16 ? 1 : 0)];
+    auto kern = r2iq_channels_v2_kernel<D, RAND, CS16, COMPACT>;
+    int &occ = g_occ[D - 4][(RAND ? 4 : 0) + (CS16 ? 2 : 0) + (COMPACT ? 1 : 0)];
     if (occ == 0) {
         int nb = 0;
         hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, NT, 0);
         if (e != hipSuccess) return e;
-        e = hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, device);
+        e = hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, L.device);
         if (e != hipSuccess) return e;
         occ = nb > 0 ? nb : 1;
     }
-    const int nframes = nblk * FRAMES;
-    const long long items = (long long)nframes * ((nch + CHUNK - 1) / CHUNK);
+    const int nframes = L.nblk * FRAMES;
+    const long long items = (long long)nframes * ((L.nch + CHUNK - 1) / CHUNK);
     const int grid = (int)(items < (long long)g_cus * occ ? items : (long long)g_cus * occ);
-    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), 0, s, reinterpret_cast<const int *>(d_in), d_out,
-                       stride / 2, nframes, d_tunebins, nch, t.tw_p1, t.rec_f, t.post8192, t.hsel[D], oa);
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), 0, L.s, reinterpret_cast<const int *>(L.d_in), L.d_out,
+                       L.stride / 2, nframes, L.d_tunebins, L.nch, t.tw_p1, t.rec_f, t.post8192, t.hsel[D], L.oa,
+                       L.windows);
     return hipGetLastError();
 }
 
-template <int D>
-hipError_t launch_d(const KernelTables &t, const int16_t *d_in, int nblk, const int *d_tunebins, int nch,
-                    void *d_out, size_t stride, OutArgs oa, int rand, int cs16, int device, hipStream_t s)
+template <int D, bool RAND, bool CS16>
+hipError_t launch_c(const KernelTables &t, const ChLaunch &L)
 {
-    if (rand)
-        return cs16 ? launch_v<D, true, true>(t, d_in, nblk, d_tunebins, nch, d_out, stride, oa, device, s)
-                    : launch_v<D, true, false>(t, d_in, nblk, d_tunebins, nch, d_out, stride, oa, device, s);
-    return cs16 ? launch_v<D, false, true>(t, d_in, nblk, d_tunebins, nch, d_out, stride, oa, device, s)
-                : launch_v<D, false, false>(t, d_in, nblk, d_tunebins, nch, d_out, stride, oa, device, s);
+    return L.windows ? launch_v<D, RAND, CS16, true>(t, L) : launch_v<D, RAND, CS16, false>(t, L);
+}
+
+template <int D>
+hipError_t launch_d(const KernelTables &t, const ChLaunch &L, int rand, int cs16)
+{
+    if (rand) return cs16 ? launch_c<D, true, true>(t, L) : launch_c<D, true, false>(t, L);
+    return cs16 ? launch_c<D, false, true>(t, L) : launch_c<D, false, false>(t, L);
 }
 
 }  // namespace
 
+bool channel_windows(int d, const int *tunebins, int nch, int2 *windows)
+{
+    const int N = HALF >> d;
+    for (int c0 = 0, k = 0; c0 < nch; c0 += CHUNK, k++) {
+        int mn = HALF, mx = -1;
+        for (int c = c0; c < c0 + CHUNK && c < nch; c++) {
+            mn = std::min(mn, tunebins[c]);
+            mx = std::max(mx, tunebins[c]);
+        }
+        const int lo = std::max(0, mn - N / 2), hi = std::min(HALF, mx + N / 2);
+        if (2 * (hi - lo) > ZC_MAX) return false;
+        windows[k] = make_int2(lo, hi - lo);
+    }
+    return true;
+}
+
 hipError_t launch_channels_v2(const KernelTables &t, int d, const int16_t *d_in, int nblk, const int *d_tunebins,
                               int nch, void *d_out, size_t stride, int lsb, int rand, int cs16, float cs16_scale,
-                              int device, hipStream_t s)
+                              const int2 *d_windows, int device, hipStream_t s)
 {
-    const OutArgs oa{lsb ? 0x80000000u : 0u, cs16_scale};
+    const ChLaunch L{d_in, nblk, d_tunebins, nch, d_out, stride, OutArgs{lsb ? 0x80000000u : 0u, cs16_scale},
+                     d_windows, device, s};
     switch (d) {
-    case 4: return launch_d<4>(t, d_in, nblk, d_tunebins, nch, d_out, stride, oa, rand, cs16, device, s);
-    case 5: return launch_d<5>(t, d_in, nblk, d_tunebins, nch, d_out, stride, oa, rand, cs16, device, s);
-    case 6: return launch_d<6>(t, d_in, nblk, d_tunebins, nch, d_out, stride, oa, rand, cs16, device, s);
+    case 4: return launch_d<4>(t, L, rand, cs16);
+    case 5: return launch_d<5>(t, L, rand, cs16);
+    case 6: return launch_d<6>(t, L, rand, cs16);
     default: return hipErrorInvalidValue;
     }
 }

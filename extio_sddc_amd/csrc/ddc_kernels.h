@@ -41,10 +41,13 @@ hipError_t launch_build_split_filter(const KernelTables &t, int d, int tunebin, 
 int channels_per_group(int d, int nch);
 
 // many-channel v2 (d = 4..6): persistent, forward once per (frame, 128-channel chunk)
-// stride: scalar components (float or int16) per channel row; cs16 as above
+// stride: scalar components (float or int16) per channel row; cs16 as above.  d_windows:
+// per-128-channel-chunk forward-bin windows from channel_windows (device copy), or nullptr.
 hipError_t launch_channels_v2(const KernelTables &t, int d, const int16_t *d_in, int nblk, const int *d_tunebins,
                               int nch, void *d_out, size_t stride, int lsb, int rand, int cs16, float cs16_scale,
-                              int device, hipStream_t s);
+                              const int2 *d_windows, int device, hipStream_t s);
+// host: the compact windows of every chunk; false if a chunk's window does not fit
+bool channel_windows(int d, const int *tunebins, int nch, int2 *windows);
 
 hipError_t launch_channels(const KernelTables &t, int d, const int16_t *d_in, int nblk,
                            const int *d_tunebins, int nch, void *d_out, size_t stride,

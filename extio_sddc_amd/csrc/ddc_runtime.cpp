@@ -101,6 +101,9 @@ struct sddc_ddc {
 
     int *d_tunebins = nullptr;             // channel tune bins (device)
     std::vector<int> tunebins_cached;
+    int2 *d_windows = nullptr;             // per-chunk compact forward-bin windows (channels v2)
+    int windows_d = -1;                    // d they were computed for; -2 = do not fit
+    hipStream_t ch_stream = nullptr;       // stream of the last many-channel launch
 
     // split x filter coefficients of the current (d, tunebin), rebuilt on device when either
     // changes; pq_used marks the last launch that read them (possibly on another stream)
@@ -280,6 +283,7 @@ int sddc_ddc_destroy(sddc_ddc_t *h)
         if (h->s_out) (void)hipStreamDestroy(h->s_out);
         for (auto &r : h->regions) (void)hipHostUnregister(const_cast<char *>(r.first));
         if (h->d_tunebins) (void)hipFree(h->d_tunebins);
+        if (h->d_windows) (void)hipFree(h->d_windows);
         if (h->d_pq) (void)hipFree(h->d_pq);
         if (h->pq_used) (void)hipEventDestroy(h->pq_used);
         for (int i = 0; i < sddc_ddc::kNcoSlots; i++) {
@@ -498,16 +502,39 @@ int sddc_ddc_process_channels_device(sddc_ddc_t *h, const int16_t *d_in, int nbl
     HIP_TRY(g.err);
     std::lock_guard<std::mutex> lk(h->mu);
     hipStream_t s = (hipStream_t)hip_stream;
-    if (h->tunebins_cached.size() != (size_t)nch ||
-        !std::equal(h->tunebins_cached.begin(), h->tunebins_cached.end(), tunebins)) {
+    const bool v2 = h->d >= 4 && h->variant == 0;
+    const bool changed = h->tunebins_cached.size() != (size_t)nch ||
+                         !std::equal(h->tunebins_cached.begin(), h->tunebins_cached.end(), tunebins);
+    if (changed || (v2 && h->windows_d != h->d && h->windows_d != -2 - 8 * h->d)) {
+        // earlier launches may still read the device copies
+        if (h->ch_stream) HIP_TRY(hipStreamSynchronize(h->ch_stream));
+        HIP_TRY(hipStreamSynchronize(s));
+    }
+    if (changed) {
         if (!h->d_tunebins) HIP_TRY(hipMalloc(&h->d_tunebins, SDDC_DDC_MAX_CHANNELS * sizeof(int)));
         h->tunebins_cached.assign(tunebins, tunebins + nch);
+        h->windows_d = -1;
         // synchronous: the host array may go away after we return
         HIP_TRY(hipMemcpy(h->d_tunebins, tunebins, nch * sizeof(int), hipMemcpyHostToDevice));
     }
-    if (h->d >= 4 && h->variant == 0)
+    const int2 *windows = nullptr;
+    if (v2) {
+        if (h->windows_d != h->d && h->windows_d != -2 - 8 * h->d) {
+            std::vector<int2> w((SDDC_DDC_MAX_CHANNELS + 127) / 128);
+            if (sddc::channel_windows(h->d, tunebins, nch, w.data())) {
+                if (!h->d_windows) HIP_TRY(hipMalloc(&h->d_windows, w.size() * sizeof(int2)));
+                HIP_TRY(hipMemcpy(h->d_windows, w.data(), w.size() * sizeof(int2), hipMemcpyHostToDevice));
+                h->windows_d = h->d;
+            } else {
+                h->windows_d = -2 - 8 * h->d;   // spread-out tune bins: full-spectrum variant
+            }
+        }
+        if (h->windows_d == h->d) windows = h->d_windows;
+    }
+    h->ch_stream = s;
+    if (v2)
         HIP_TRY(sddc::launch_channels_v2(h->tables, h->d, d_in, nblk, h->d_tunebins, nch, d_out, out_stride,
-                                         h->lsb, h->rand, cs16, h->cs16_scale, h->device, s));
+                                         h->lsb, h->rand, cs16, h->cs16_scale, windows, h->device, s));
     else
         HIP_TRY(sddc::launch_channels(h->tables, h->d, d_in, nblk, h->d_tunebins, nch, d_out, out_stride,
                                       h->lsb, h->rand, cs16, h->cs16_scale, s));
