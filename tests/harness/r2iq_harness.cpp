@@ -5,9 +5,11 @@
 // thread collects the 32768-sample output blocks into a file.  Also probes the base-class
 // byte layout of the private fields (randADC @44, sideband @45, Core/r2iq.h).
 //
-//   r2iq_harness IN.bin NBLK D TUNEBIN LSB RAND GAIN OUT.bin
+//   r2iq_harness IN.bin NBLK D TUNEBIN LSB RAND GAIN OUT.bin [CYCLES]
 // OUT.bin "-" discards the IQ and reports the end-to-end input rate (PCIe + host copies
-// included); IN.bin may hold fewer blocks than NBLK, it is then cycled.
+// included); IN.bin may hold fewer blocks than NBLK, it is then cycled.  CYCLES > 1 repeats
+// TurnOn -> NBLK blocks -> TurnOff on the same object and rings (the Start/Stop cycling of
+// unittest/stability_test.cpp:255-301); each cycle's IQ is appended to OUT.bin.
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -20,10 +22,11 @@
 
 int main(int argc, char **argv)
 {
-    if (argc != 9) {
-        std::fprintf(stderr, "usage: %s IN.bin NBLK D TUNEBIN LSB RAND GAIN OUT.bin\n", argv[0]);
+    if (argc != 9 && argc != 10) {
+        std::fprintf(stderr, "usage: %s IN.bin NBLK D TUNEBIN LSB RAND GAIN OUT.bin [CYCLES]\n", argv[0]);
         return 2;
     }
+    const int cycles = argc == 10 ? std::atoi(argv[9]) : 1;
     const int nblk = std::atoi(argv[2]), d = std::atoi(argv[3]), tb = std::atoi(argv[4]);
     const bool lsb = std::atoi(argv[5]) != 0, rnd = std::atoi(argv[6]) != 0;
     const float gain = (float)std::atof(argv[7]);
@@ -56,36 +59,41 @@ int main(int argc, char **argv)
         return 5;
     }
     const float fc = base->setFreqOffset((float)tb / 4096.0f);
-    base->TurnOn();
-    if (!base->IsOn()) {
-        std::fprintf(stderr, "TurnOn failed: %s\n", r.lastError());
-        return 3;
-    }
-    std::thread producer([&] {
-        for (int b = 0; b < nblk; b++) {
-            int16_t *p = inbuf.getWritePtr();
-            if (!base->IsOn()) return;
-            std::memcpy(p, data.data() + (size_t)(b % have) * 65536, 65536 * sizeof(int16_t));
-            inbuf.WriteDone();
-        }
-    });
     FILE *out = discard ? nullptr : std::fopen(argv[8], "wb");
     const int want = nblk >> d;
     int got = 0;
-    const auto t0 = std::chrono::steady_clock::now();
-    for (; got < want; got++) {
-        const float *p = outbuf.getReadPtr();
-        if (!base->IsOn()) break;
-        if (out) fwrite(p, sizeof(float), 65536, out);
-        outbuf.ReadDone();
+    for (int cyc = 0; cyc < cycles; cyc++) {
+        base->TurnOn();
+        if (!base->IsOn()) {
+            std::fprintf(stderr, "TurnOn failed: %s\n", r.lastError());
+            return 3;
+        }
+        std::thread producer([&] {
+            for (int b = 0; b < nblk; b++) {
+                int16_t *p = inbuf.getWritePtr();
+                if (!base->IsOn()) return;
+                std::memcpy(p, data.data() + (size_t)(b % have) * 65536, 65536 * sizeof(int16_t));
+                inbuf.WriteDone();
+            }
+        });
+        got = 0;
+        const auto t0 = std::chrono::steady_clock::now();
+        for (; got < want; got++) {
+            const float *p = outbuf.getReadPtr();
+            if (!base->IsOn()) break;
+            if (out) fwrite(p, sizeof(float), 65536, out);
+            outbuf.ReadDone();
+        }
+        const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (discard)
+            std::printf("end-to-end: %d blocks in %.3f s = %.1f input MS/s\n", nblk, secs,
+                        nblk * 65536.0 / secs / 1e6);
+        base->TurnOff();
+        producer.join();
+        std::printf("cycle %d: output blocks %d of %d, residual fc %g, gpu blocks %llu\n", cyc, got, want, fc,
+                    (unsigned long long)r.blocksProcessed());
+        if (got != want) break;
     }
-    const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     if (out) std::fclose(out);
-    if (discard)
-        std::printf("end-to-end: %d blocks in %.3f s = %.1f input MS/s\n", nblk, secs, nblk * 65536.0 / secs / 1e6);
-    base->TurnOff();
-    producer.join();
-    std::printf("output blocks %d of %d, residual fc %g, gpu blocks %llu\n", got, want, fc,
-                (unsigned long long)r.blocksProcessed());
     return got == want ? 0 : 4;
 }

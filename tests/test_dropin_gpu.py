@@ -89,3 +89,20 @@ def test_reference_radiohandler_fine_tune(tmp_path, oracle, srate_idx, tune_hz, 
     ref = oracle.Nco(fc).apply(plain)
     assert y.size == ref.size
     assert oracle.max_rel_err(y, ref) <= TOL
+
+
+def test_dropin_start_stop_cycles(tmp_path, oracle):
+    """20 TurnOn/TurnOff cycles on one object and one pair of rings (the Start/Stop cycling of
+    unittest/stability_test.cpp:255-301): every cycle restarts from a zero history
+    (TurnOn, fft_mt_r2iq.cpp:111-129), so each cycle's IQ equals the oracle's."""
+    d, tb, nblk, cycles = 1, 1024, 8, 20
+    x = make_stream(nblk, "mix")
+    fin, fout = tmp_path / "in.bin", tmp_path / "out.bin"
+    x[4096:].tofile(fin)
+    out = _run([HARNESS, str(fin), str(nblk), str(d), str(tb), "0", "0", "1.0", str(fout), str(cycles)])
+    assert out.count("output blocks 4 of 4") == cycles, out
+    y = np.fromfile(fout, np.float32).view(np.complex64).reshape(cycles, -1)
+    ref = oracle.r2iq(x, nblk, d, tb)
+    for c in range(cycles):
+        assert oracle.max_rel_err(y[c], ref) <= TOL
+        np.testing.assert_array_equal(y[c].view(np.uint32), y[0].view(np.uint32))

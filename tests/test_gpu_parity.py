@@ -243,3 +243,28 @@ def test_block_limit_and_empty_calls(torch_dev, ddc):
             check(ddc._L.sddc_ddc_process_device(ddc._h, x.data_ptr(), bad, y.data_ptr(), None))
     with pytest.raises(DDCError):
         ddc.process(np.zeros(0, np.int16))
+
+
+def test_max_blocks_one_launch(torch_dev, ddc):
+    """SDDC_DDC_MAX_BLOCKS (32768 blocks = 2^31 samples, 4 GiB in, 8 GiB out) in one launch
+    equals the same stream as two halo'd halves, bit-exact; nothing is left unwritten."""
+    torch = torch_dev
+    from extio_sddc_amd import output_samples
+    nblk, half = 32768, 16384
+    g = torch.Generator(device="cuda").manual_seed(0x5DDC + 1)
+    d_in = torch.randint(-32768, 32767, (4096 + nblk * 65536,), dtype=torch.int16, device="cuda", generator=g)
+    ddc.setDecimate(0)
+    ddc.setTuneBin(1024)
+    ddc.setSideband(False)
+    ddc.updateRand(False)
+    n = output_samples(0, nblk) * 2
+    full = torch.full((n,), float("nan"), dtype=torch.float32, device="cuda")
+    ddc.process_device(d_in, nblk, full)
+    parts = torch.full((n,), float("nan"), dtype=torch.float32, device="cuda")
+    ddc.process_device(d_in, half, parts[: n // 2])
+    ddc.process_device(d_in[half * 65536:], half, parts[n // 2:])
+    torch.cuda.synchronize()
+    assert torch.isfinite(full).all()
+    assert torch.equal(full, parts)
+    del d_in, full, parts
+    torch.cuda.empty_cache()
