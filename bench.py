@@ -156,7 +156,8 @@ def main() -> None:
     # launches run ~20 % slower; 50 + 100 steps of 2048 blocks take ~50 ms
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=50)
-    ap.add_argument("--d", type=int, default=0, help="decimation index (0 = decim 2)")
+    ap.add_argument("--d", "--decim-index", dest="d", type=int, default=0,
+                    help="decimation index (0 = decim 2); use --decim-index under torchrun")
     ap.add_argument("--tunebin", type=int, default=1024)
     ap.add_argument("--nblk", type=int, default=2048, help="blocks of 65536 per step per GPU")
     ap.add_argument("--mode", choices=["single", "channels"], default="single")
@@ -180,14 +181,22 @@ def main() -> None:
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # one rank per GPU; SDDC_BENCH_BACKEND=gloo lets a rehearsal put several ranks on one GPU
+    # (RCCL refuses two ranks on one device); the driver's runs use the default, RCCL
+    backend = os.environ.get("SDDC_BENCH_BACKEND", "nccl")
+    ngpu = torch.cuda.device_count()
+    gpu = local % ngpu if backend == "gloo" else local
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     d, nblk = args.d, args.nblk
-    ddc = R2iq(gain=1.0, device=local)
+    ddc = R2iq(gain=1.0, device=gpu)
     ddc.setDecimate(d)
     ddc.setTuneBin(args.tunebin)
     if args.fine_tune:
@@ -250,7 +259,7 @@ def main() -> None:
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     kern_ms = ev0.elapsed_time(ev1) / args.steps          # per step on the launch stream
-    t = torch.tensor([wall, kern_ms], dtype=torch.float64, device=dev)
+    t = torch.tensor([wall, kern_ms], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall, kern_ms = t.tolist()
