@@ -1,12 +1,15 @@
 /*
- * sddc_compat/fft_backend.h — standalone stand-in for ExtIO_sddc's FFT backend interface
- * (Core/fft_backend.h:1-59), used ONLY when this repository is built without the
- * ExtIO_sddc tree (tests, the GPU box).  In the integration build the reference's own
- * header is found first and this file is never seen.
+ * sddc_compat/fft_backend.h
  *
- * Restates the same interface: the abstract class FFTBackend with the same virtual
- * functions in the same declaration order (so the Itanium vtable layout matches), the
- * FFTPlanHandle / FFTDirection / fft_complex types and the getFFTBackend() factory.
+ * Used only for builds of this repository WITHOUT the ExtIO_sddc tree.  The integration
+ * build compiles extio_sddc_amd/csrc/fft_backend/fft_backend_hip.cpp against the tree's own
+ * Core/fft_backend.h instead.
+ *
+ * What it must preserve (Core/fft_backend.h:1-59): the abstract plan/execute interface the
+ * tree's fft_benchmark.cpp drives, with the virtual functions in the same declaration order
+ * (so the Itanium vtables agree): destructor, name, plan_r2c, plan_c2c, execute_r2c,
+ * execute_c2c, destroy_plan, import_wisdom, export_wisdom, alloc, free; the plan handle,
+ * direction and complex types; and the getFFTBackend() factory the build links in.
  */
 #ifndef SDDC_COMPAT_FFT_BACKEND_H
 #define SDDC_COMPAT_FFT_BACKEND_H
@@ -15,27 +18,35 @@
 #include <complex>
 #include <cstddef>
 
-using fft_complex = std::complex<float>;   /* interleaved (re, im), fftwf_complex compatible */
-typedef void *FFTPlanHandle;
+using fft_complex = std::complex<float>; // (re, im) pairs, layout-compatible with fftwf_complex
+typedef void *FFTPlanHandle;             // owned by the backend that created it
 
 enum class FFTDirection { Forward, Backward };
 
-class FFTBackend {
+class FFTBackend
+{
 public:
     virtual ~FFTBackend() = default;
+
     virtual const char *name() const = 0;
-    virtual FFTPlanHandle plan_r2c(int n, float *in, fft_complex *out) = 0;
-    virtual FFTPlanHandle plan_c2c(int n, fft_complex *in, fft_complex *out, FFTDirection dir) = 0;
-    virtual void execute_r2c(FFTPlanHandle plan, float *in, fft_complex *out) = 0;
-    virtual void execute_c2c(FFTPlanHandle plan, fft_complex *in, fft_complex *out) = 0;
-    virtual void destroy_plan(FFTPlanHandle plan) = 0;
-    virtual void import_wisdom(const char *filename) { (void)filename; }
-    virtual void export_wisdom(const char *filename) { (void)filename; }
-    virtual void *alloc(size_t bytes) = 0;
-    virtual void free(void *ptr) = 0;
+
+    // plans remember size (and direction); execute may be handed other arrays of that size
+    virtual FFTPlanHandle plan_r2c(int size, float *realIn, fft_complex *binsOut) = 0;
+    virtual FFTPlanHandle plan_c2c(int size, fft_complex *src, fft_complex *dst, FFTDirection sign) = 0;
+    virtual void execute_r2c(FFTPlanHandle p, float *realIn, fft_complex *binsOut) = 0;
+    virtual void execute_c2c(FFTPlanHandle p, fft_complex *src, fft_complex *dst) = 0;
+    virtual void destroy_plan(FFTPlanHandle p) = 0;
+
+    // FFTW wisdom files; other backends ignore them
+    virtual void import_wisdom(const char *path) { (void)path; }
+    virtual void export_wisdom(const char *path) { (void)path; }
+
+    // buffers the backend can transform in place of its caller's (alignment, pinning)
+    virtual void *alloc(size_t nbytes) = 0;
+    virtual void free(void *mem) = 0;
 };
 
-FFTBackend *getFFTBackend();
+FFTBackend *getFFTBackend(); // the one backend linked into this build
 
 #define FFT_BACKEND_NAME "HIP"
 

@@ -1,18 +1,30 @@
 /*
- * sddc_compat/r2iq.h — standalone stand-in for the ExtIO_sddc boundary class, used ONLY
- * when this repository is built without the ExtIO_sddc tree (tests, the GPU box).
+ * sddc_compat/r2iq.h
  *
- * In the integration build the reference's own Core/r2iq.h is first on
- * the include path and this file is never seen.  It restates the interface of
- * r2iqControlClass (Core/r2iq.h:16-48) with an identical object layout, so code
- * compiled against either header is ABI-compatible (x86-64 Itanium ABI: vptr @0,
- * mdecimation @8, r2iqOn @12, mratio[7] @16, randADC @44, sideband @45, sizeof 48;
- * checked by static_asserts in extio_sddc_amd/csrc/r2iq/fft_mt_r2iq.cpp).
+ * Used only for builds of this repository WITHOUT the ExtIO_sddc tree (the tests, the GPU
+ * box).  In the integration build the tree's Core/r2iq.h comes first on the include path
+ * and this file is not seen.
+ *
+ * What it must preserve: the object layout and vtable of the boundary base class described
+ * in SURVEY.md §8(b) (Core/r2iq.h:16-48), so a caller compiled against either header talks
+ * to the same object.  Itanium x86-64 layout, checked by static_asserts in
+ * extio_sddc_amd/csrc/r2iq/fft_mt_r2iq.cpp and by the byte probe in tests/harness:
+ *
+ *     offset  0  vptr
+ *     offset  8  int   decimation index
+ *     offset 12  bool  running flag
+ *     offset 16  int   ratio table [7]
+ *     offset 44  bool  RAND de-randomisation
+ *     offset 45  bool  lower-sideband conjugation          sizeof = 48
+ *
+ * Virtual slots, in order: destructor (complete, deleting), Init, TurnOn, TurnOff, IsOn,
+ * DataReady, setFreqOffset.  The small setters and getters are non-virtual inlines, so they
+ * compile into the caller and only touch the fields above.
  */
 #ifndef R2IQ_H
 #define R2IQ_H
 
-#define NDECIDX 7  /* number of decimation ratios, r2iq.h:5 */
+#define NDECIDX 7 /* decimation indices 0..6 */
 
 #include <atomic>
 #include <condition_variable>
@@ -23,35 +35,36 @@
 
 struct r2iqThreadArg;
 
-class r2iqControlClass {
+class r2iqControlClass
+{
 public:
-    r2iqControlClass();                 /* defined by the DDC implementation (fft_mt_r2iq.cpp) */
+    r2iqControlClass(); // out of line, supplied by the DDC (extio_sddc_amd/csrc/r2iq/fft_mt_r2iq.cpp)
     virtual ~r2iqControlClass() {}
 
-    /* non-virtual accessors, inlined into callers such as RadioHandler */
+    // -- inline field accessors (caller-side code) --
     int getRatio() { return mratio[mdecimation]; }
-    void updateRand(bool v) { randADC = v; }
+    void updateRand(bool on) { randADC = on; }
     bool getRand() const { return randADC; }
-    void setSideband(bool lsb) { sideband = lsb; }
+    void setSideband(bool lower) { sideband = lower; }
     bool getSideband() const { return sideband; }
-    void setDecimate(int dec) { mdecimation = dec; }
+    void setDecimate(int index) { mdecimation = index; }
 
-    /* virtual interface, vtable order as in the reference */
-    virtual void Init(float gain, ringbuffer<int16_t> *input, ringbuffer<float> *obuffers) {}
+    // -- virtual interface (slot order fixed by the ABI) --
+    virtual void Init(float gainScale, ringbuffer<int16_t> *samplesIn, ringbuffer<float> *iqOut) {}
     virtual void TurnOn() { r2iqOn = true; }
     virtual void TurnOff(void) { r2iqOn = false; }
     virtual bool IsOn(void) { return r2iqOn; }
     virtual void DataReady(void) {}
-    virtual float setFreqOffset(float offset) { return 0; }
+    virtual float setFreqOffset(float fractionOfHalfRate) { return 0; }
 
 protected:
-    int mdecimation;        /* 0..6: output rate = ADC rate / 2^(d+1) */
-    bool r2iqOn;
-    int mratio[NDECIDX];    /* 2^d */
+    int mdecimation;     // output rate = ADC rate / 2^(index + 1)
+    bool r2iqOn;         // set by TurnOn, cleared by TurnOff
+    int mratio[NDECIDX]; // 1, 2, 4, ... 64
 
 private:
-    bool randADC;           /* ADC RAND mode: de-randomise on conversion */
-    bool sideband;          /* true: conjugate the IQ (lower sideband) */
+    bool randADC;        // odd samples arrive XORed with 0xFFFE
+    bool sideband;       // conjugate the output
 };
 
-#endif
+#endif /* R2IQ_H */
