@@ -44,7 +44,8 @@ constexpr bool kDB = SDDC_DB != 0;
 #endif
 #ifndef SDDC_FAKE
 #define SDDC_FAKE 0           // timing-only builds: 1 = no filter/PQ loads, 2 = no pass-1 twiddle reads,
-                              // 4 = no loop barriers, 8 = no output stores, 16 = no input loads
+                              // 4 = no loop barriers, 8 = no output stores, 16 = no input loads,
+                              // 32 = no LDS exchange reads (N >= 512), 64 = no LDS exchange writes (N >= 512)
 #endif
 #ifndef SDDC_PQ
 #define SDDC_PQ 1             // split x filter from the per-(d, tunebin) coefficient table (P, Q)
@@ -73,6 +74,8 @@ __device__ constexpr float kW32im[32] = {
     5.555702330e-01f, 3.826834324e-01f, 1.950903220e-01f};
 
 #define LOOP_SYNC() do { if constexpr (!(SDDC_FAKE & 4)) __syncthreads(); } while (0)
+#define LDS_RD(expr, fake) ((SDDC_FAKE & 32) ? (fake) : (expr))
+#define LDS_WR if constexpr (!(SDDC_FAKE & 64))
 
 __device__ __forceinline__ int swz(int e) { return e ^ ((e >> 4) & 15); }
 
@@ -301,13 +304,13 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
         }
         if constexpr (!kDB) LOOP_SYNC();   // the previous frame's last LDS reads are done
 #pragma unroll
-        for (int r = 0; r < 16; r++) w0[16 * t + (r ^ x15)] = v[r];          // swz(16t + r)
+        for (int r = 0; r < 16; r++) LDS_WR w0[16 * t + (r ^ x15)] = v[r];          // swz(16t + r)
         LOOP_SYNC();
         // ---- forward pass 1 (R16, NS16): table twiddles W_256^{(t%16) r} ----
         {
             float2 a[16];
 #pragma unroll
-            for (int r = 0; r < 16; r++) a[r] = w0[sT + NT * r];
+            for (int r = 0; r < 16; r++) a[r] = LDS_RD(w0[sT + NT * r], v[r]);
 #pragma unroll
             for (int r = 1; r < 16; r++)
                 a[r] = TW<-1>(a[r], (SDDC_FAKE & 2) ? make_float2(0.7f, 0.01f * (r + x15)) : twl[(r - 1) * 16 + x15]);
@@ -317,14 +320,14 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
         {
             const int b1 = (t >> 4) * 256;                                     // swz(b1 + x15 + 16 r)
 #pragma unroll
-            for (int r = 0; r < 16; r++) w1[b1 + 16 * r + (x15 ^ r)] = v[r];
+            for (int r = 0; r < 16; r++) LDS_WR w1[b1 + 16 * r + (x15 ^ r)] = v[r];
         }
         LOOP_SYNC();
         // ---- forward pass 2 (R16, NS256): recurrence twiddles W_4096^{t r} ----
         {
             float2 a[16];
 #pragma unroll
-            for (int r = 0; r < 16; r++) a[r] = w1[sT + NT * r];
+            for (int r = 0; r < 16; r++) a[r] = LDS_RD(w1[sT + NT * r], v[r]);
             if constexpr (SDDC_TWTAB) {
 #pragma unroll
                 for (int r = 1; r < 16; r++) a[r] = TW<-1>(a[r], ttf[(r - 1) * NT + t]);
@@ -335,7 +338,7 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
         }
         if constexpr (!kDB) LOOP_SYNC();
 #pragma unroll
-        for (int r = 0; r < 16; r++) w0[sT + NT * r] = v[r];   // Z, natural order
+        for (int r = 0; r < 16; r++) LDS_WR w0[sT + NT * r] = v[r];   // Z, natural order
         LOOP_SYNC();
 
         if constexpr (N >= 512) {
@@ -359,10 +362,10 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
                     // branch-free: read a valid (wrapped) address; out-of-band bins have P = Q = 0
                     if constexpr (SDDC_PQ) {
                         // byte offsets: the wrap is one AND, the scale folds away
-                        const float2 zk = *reinterpret_cast<const float2 *>(
-                            w0b + ((sb0b + 8u * (unsigned)sh) & (8u * HALF - 8u)));
-                        const float2 zc = *reinterpret_cast<const float2 *>(
-                            w0b + ((sc0b - 8u * (unsigned)sh) & (8u * HALF - 8u)));
+                        const float2 zk = LDS_RD(*reinterpret_cast<const float2 *>(
+                            w0b + ((sb0b + 8u * (unsigned)sh) & (8u * HALF - 8u))), v[r]);
+                        const float2 zc = LDS_RD(*reinterpret_cast<const float2 *>(
+                            w0b + ((sc0b - 8u * (unsigned)sh) & (8u * HALF - 8u))), v[(r + 1) & 15]);
                         float4 c;
                         if constexpr (SDDC_FAKE & 1)
                             c = make_float4(0.5f, 0.25f * r, 0.1f, 0.2f);
@@ -389,7 +392,7 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
             if constexpr (!kDB) LOOP_SYNC();
             if constexpr (R0 == 16) {
 #pragma unroll
-                for (int r = 0; r < 16; r++) w1[16 * t + (r ^ x15)] = u[r];
+                for (int r = 0; r < 16; r++) LDS_WR w1[16 * t + (r ^ x15)] = u[r];
             } else {
 #pragma unroll
                 for (int r = 0; r < R0; r++) w1[swz(R0 * t + r)] = u[r];
@@ -402,7 +405,7 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
                 float2 a[16];
                 if constexpr (NB == NT) {
 #pragma unroll
-                    for (int r = 0; r < 16; r++) a[r] = w1[sT + NT * r];
+                    for (int r = 0; r < 16; r++) a[r] = LDS_RD(w1[sT + NT * r], u[r]);
                 } else {
 #pragma unroll
                     for (int r = 0; r < 16; r++) a[r] = w1[swz(t + NB * r)];
@@ -417,7 +420,7 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
                 if constexpr (R0 == 16) {
                     const int b1 = (t >> 4) * 256;
 #pragma unroll
-                    for (int r = 0; r < 16; r++) w0[b1 + 16 * r + (x15 ^ r)] = u[r];
+                    for (int r = 0; r < 16; r++) LDS_WR w0[b1 + 16 * r + (x15 ^ r)] = u[r];
                 } else {
                     const int base = (t / R0) * (16 * R0) + (t % R0);
 #pragma unroll
@@ -430,7 +433,7 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
                 float2 a[16];
                 if constexpr (NB == NT) {
 #pragma unroll
-                    for (int r = 0; r < 16; r++) a[r] = w0[sT + NT * r];
+                    for (int r = 0; r < 16; r++) a[r] = LDS_RD(w0[sT + NT * r], u[r]);
                 } else {
 #pragma unroll
                     for (int r = 0; r < 16; r++) a[r] = w0[swz(t + NB * r)];
