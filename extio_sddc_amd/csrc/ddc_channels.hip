@@ -33,6 +33,9 @@ constexpr int ZC_MAX = 1536;  // compact window of forward bins per chunk (windo
 
 __device__ __forceinline__ int swz(int e) { return e ^ ((e >> 4) & 15); }
 
+#ifndef SDDC_CH_NT
+#define SDDC_CH_NT 1          // non-temporal IQ stores
+#endif
 #ifndef SDDC_CH_WAVESYNC
 #define SDDC_CH_WAVESYNC 1   // the per-channel exchange is wave-local: order it within the wave only
 #endif
@@ -238,11 +241,18 @@ __global__ __launch_bounds__(NT, 2) void r2iq_channels_v2_kernel(
             // pass B: radix-RB Stockham step (NS = 16), twiddles W_N^{j q} = W_256^{(256/N) j q}
             if (cok) {
                 char *ob = static_cast<char *>(out) + ((size_t)c * stride + (size_t)blk * 8 * N) * out_bytes<CS16>();
-                auto put = [&](int idx, float2 o) {
-                    if constexpr (CS16)
-                        reinterpret_cast<unsigned *>(ob)[idx] = cs16_pack(o, oa.scale);
-                    else
-                        reinterpret_cast<float2 *>(ob)[idx] = o;
+                auto put = [&](int idx, float2 o) {   // streaming (nt) stores, as the single-channel kernel's
+                    if constexpr (CS16) {
+                        unsigned *p = reinterpret_cast<unsigned *>(ob) + idx;
+                        if constexpr (SDDC_CH_NT) __builtin_nontemporal_store(cs16_pack(o, oa.scale), p);
+                        else *p = cs16_pack(o, oa.scale);
+                    } else {
+                        typedef float f2x __attribute__((ext_vector_type(2)));
+                        f2x *p = reinterpret_cast<f2x *>(ob) + idx;
+                        const f2x v = {o.x, o.y};
+                        if constexpr (SDDC_CH_NT) __builtin_nontemporal_store(v, p);
+                        else *p = v;
+                    }
                 };
 #pragma unroll
                 for (int b = 0; b < BPT; b++) {

@@ -53,6 +53,12 @@ constexpr bool kDB = SDDC_DB != 0;
 #ifndef SDDC_PK
 #define SDDC_PK 0             // 1: radix-16 DFTs and twiddle products in packed FP32 (measured slower)
 #endif
+#ifndef SDDC_PAD
+#define SDDC_PAD 0            // 1: 17-per-16 padded LDS rows for the radix-16 exchanges (no address VGPRs)
+#endif
+#ifndef SDDC_TWREG
+#define SDDC_TWREG 0          // bit d set: at decimation d the pass-2 twiddles W_4096^{t r} stay in 30 VGPRs
+#endif
 #ifndef SDDC_PREFETCH
 #define SDDC_PREFETCH 1       // load the next frame's input during the current one
 #endif
@@ -229,7 +235,7 @@ __device__ __forceinline__ void load_frame(const int *__restrict__ in32, int blk
     const __amdgpu_buffer_rsrc_t rs = buf_rsrc(in32 + ((size_t)blk * BLOCK + (size_t)k * HOP) / 2);
     const unsigned vo = 4u * threadIdx.x;
 #pragma unroll
-    for (int r = 0; r < 16; r++) x[r] = buf_load4(rs, vo, 4u * NT * r);
+    for (int r = 0; r < 16; r++) x[r] = buf_load4<SDDC_LD_AUX>(rs, vo, 4u * NT * r);
 }
 
 template <int D, bool RAND, bool NCO, bool CS16>
@@ -242,11 +248,12 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
     const float4 *__restrict__ pq, int tunebin, OutArgs oa, NcoArgs nco)
 {
     constexpr int N = HALF >> D;
-    __shared__ __attribute__((aligned(16))) float2 lds[kDB ? 2 * HALF : HALF];
+    constexpr int LDSN = SDDC_PAD ? HALF + HALF / 16 : HALF;   // padded: element e at e + e/16
+    __shared__ __attribute__((aligned(16))) float2 lds[kDB ? 2 * LDSN : LDSN];
     // pass-1 twiddle tables, copied once per workgroup: [15][16] forward, [15][S] inverse
     constexpr int SQ = N >= 512 ? N / 256 : N / 16;
     __shared__ __attribute__((aligned(16))) float2 twl[15 * 16 + 15 * SQ];
-    float2 *w0 = lds, *w1 = kDB ? lds + HALF : lds;   // this frame's pass buffers
+    float2 *w0 = lds, *w1 = kDB ? lds + LDSN : lds;   // this frame's pass buffers
 
     const int tid = (int)threadIdx.x;
     const int G = (int)gridDim.x, w = (int)blockIdx.x;
@@ -264,6 +271,12 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
         }
     }
     const float2 pb_ = post8192[(tunebin + tid) & 8191];   // W_8192^{tb + tid}
+    constexpr bool kTwReg = (SDDC_TWREG >> D) & 1;
+    float2 twr[kTwReg ? 15 : 1];                            // W_4096^{tid r}, r = 1..15 (exact table values)
+    if constexpr (kTwReg) {
+#pragma unroll
+        for (int r = 1; r < 16; r++) twr[r - 1] = twt_f[(r - 1) * NT + tid];
+    }
     for (int i = tid; i < 15 * 16 + 15 * SQ; i += NT)
         twl[i] = i < 15 * 16 ? tw_p1[i] : tw_q1[i - 15 * 16];   // visible after the first frame's pass-0 barrier
 
@@ -284,6 +297,8 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
         float2 fw1 = fw1_, fw4 = fw4_, iw1 = iw1_, iw4 = iw4_, pb = pb_;
         asm volatile("" : "+v"(fw1), "+v"(fw4), "+v"(iw1), "+v"(iw4), "+v"(pb));
         const int sT = swz(t);            // swz(t + 256 r) = sT + 256 r
+        const int pT = t + (t >> 4);      // padded: P(t + 256 r) = pT + 272 r
+        constexpr int PR = NT + NT / 16;
         const int x15 = t & 15;
         const int oblk = blk * 8 * N;   // first output slot of the block (batch-relative)
         const int kc = k;
@@ -304,13 +319,13 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
         }
         if constexpr (!kDB) LOOP_SYNC();   // the previous frame's last LDS reads are done
 #pragma unroll
-        for (int r = 0; r < 16; r++) LDS_WR w0[16 * t + (r ^ x15)] = v[r];          // swz(16t + r)
+        for (int r = 0; r < 16; r++) LDS_WR w0[SDDC_PAD ? 17 * t + r : 16 * t + (r ^ x15)] = v[r];   // P or swz(16t + r)
         LOOP_SYNC();
         // ---- forward pass 1 (R16, NS16): table twiddles W_256^{(t%16) r} ----
         {
             float2 a[16];
 #pragma unroll
-            for (int r = 0; r < 16; r++) a[r] = LDS_RD(w0[sT + NT * r], v[r]);
+            for (int r = 0; r < 16; r++) a[r] = LDS_RD(SDDC_PAD ? w0[pT + PR * r] : w0[sT + NT * r], v[r]);
 #pragma unroll
             for (int r = 1; r < 16; r++)
                 a[r] = TW<-1>(a[r], (SDDC_FAKE & 2) ? make_float2(0.7f, 0.01f * (r + x15)) : twl[(r - 1) * 16 + x15]);
@@ -320,15 +335,18 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
         {
             const int b1 = (t >> 4) * 256;                                     // swz(b1 + x15 + 16 r)
 #pragma unroll
-            for (int r = 0; r < 16; r++) LDS_WR w1[b1 + 16 * r + (x15 ^ r)] = v[r];
+            for (int r = 0; r < 16; r++) LDS_WR w1[SDDC_PAD ? (t >> 4) * 272 + x15 + 17 * r : b1 + 16 * r + (x15 ^ r)] = v[r];
         }
         LOOP_SYNC();
         // ---- forward pass 2 (R16, NS256): recurrence twiddles W_4096^{t r} ----
         {
             float2 a[16];
 #pragma unroll
-            for (int r = 0; r < 16; r++) a[r] = LDS_RD(w1[sT + NT * r], v[r]);
-            if constexpr (SDDC_TWTAB) {
+            for (int r = 0; r < 16; r++) a[r] = LDS_RD(SDDC_PAD ? w1[pT + PR * r] : w1[sT + NT * r], v[r]);
+            if constexpr (kTwReg) {
+#pragma unroll
+                for (int r = 1; r < 16; r++) a[r] = TW<-1>(a[r], twr[r - 1]);
+            } else if constexpr (SDDC_TWTAB) {
 #pragma unroll
                 for (int r = 1; r < 16; r++) a[r] = TW<-1>(a[r], ttf[(r - 1) * NT + t]);
             } else {
@@ -392,7 +410,7 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
             if constexpr (!kDB) LOOP_SYNC();
             if constexpr (R0 == 16) {
 #pragma unroll
-                for (int r = 0; r < 16; r++) LDS_WR w1[16 * t + (r ^ x15)] = u[r];
+                for (int r = 0; r < 16; r++) LDS_WR w1[SDDC_PAD ? 17 * t + r : 16 * t + (r ^ x15)] = u[r];
             } else {
 #pragma unroll
                 for (int r = 0; r < R0; r++) w1[swz(R0 * t + r)] = u[r];
@@ -405,7 +423,7 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
                 float2 a[16];
                 if constexpr (NB == NT) {
 #pragma unroll
-                    for (int r = 0; r < 16; r++) a[r] = LDS_RD(w1[sT + NT * r], u[r]);
+                    for (int r = 0; r < 16; r++) a[r] = LDS_RD(SDDC_PAD ? w1[pT + PR * r] : w1[sT + NT * r], u[r]);
                 } else {
 #pragma unroll
                     for (int r = 0; r < 16; r++) a[r] = w1[swz(t + NB * r)];
@@ -420,7 +438,7 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
                 if constexpr (R0 == 16) {
                     const int b1 = (t >> 4) * 256;
 #pragma unroll
-                    for (int r = 0; r < 16; r++) LDS_WR w0[b1 + 16 * r + (x15 ^ r)] = u[r];
+                    for (int r = 0; r < 16; r++) LDS_WR w0[SDDC_PAD ? (t >> 4) * 272 + x15 + 17 * r : b1 + 16 * r + (x15 ^ r)] = u[r];
                 } else {
                     const int base = (t / R0) * (16 * R0) + (t % R0);
 #pragma unroll
@@ -433,12 +451,15 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
                 float2 a[16];
                 if constexpr (NB == NT) {
 #pragma unroll
-                    for (int r = 0; r < 16; r++) a[r] = LDS_RD(w0[sT + NT * r], u[r]);
+                    for (int r = 0; r < 16; r++) a[r] = LDS_RD(SDDC_PAD ? w0[pT + PR * r] : w0[sT + NT * r], u[r]);
                 } else {
 #pragma unroll
                     for (int r = 0; r < 16; r++) a[r] = w0[swz(t + NB * r)];
                 }
-                if constexpr (SDDC_TWTAB) {
+                if constexpr (kTwReg && N == HALF) {
+#pragma unroll
+                    for (int r = 1; r < 16; r++) a[r] = TW<+1>(a[r], twr[r - 1]);
+                } else if constexpr (SDDC_TWTAB) {
 #pragma unroll
                     for (int r = 1; r < 16; r++) a[r] = TW<+1>(a[r], (N == HALF ? ttf : tti)[(r - 1) * NB + t]);
                 } else {
