@@ -73,44 +73,11 @@ __device__ constexpr float kW32im[32] = {
     9.807852804e-01f, 1.0f, 9.807852804e-01f, 9.238795325e-01f, 8.314696123e-01f, 7.071067812e-01f,
     5.555702330e-01f, 3.826834324e-01f, 1.950903220e-01f};
 
-#define LOOP_SYNC() do { if constexpr (!(SDDC_FAKE & 4)) __syncthreads(); if constexpr (SDDC_WPRIO > 0) __builtin_amdgcn_s_setprio(0); } while (0)
+#define LOOP_SYNC() do { if constexpr (!(SDDC_FAKE & 4)) __syncthreads(); } while (0)
 #define LDS_RD(expr, fake) ((SDDC_FAKE & 32) ? (fake) : (expr))
 #define LDS_WR if constexpr (!(SDDC_FAKE & 64))
-#ifndef SDDC_PRIO
-#define SDDC_PRIO 0           // >0: raised wave priority while a wave issues an exchange's reads
-#endif
-#ifndef SDDC_WPRIO
-#define SDDC_WPRIO 0          // >0: raised wave priority from an exchange's writes until its barrier
-#endif
-#define PRIO(p) do { if constexpr (SDDC_PRIO > 0) __builtin_amdgcn_s_setprio(p); } while (0)
-#define WPRIO() do { if constexpr (SDDC_WPRIO > 0) __builtin_amdgcn_s_setprio(SDDC_WPRIO); } while (0)
 
 __device__ __forceinline__ int swz(int e) { return e ^ ((e >> 4) & 15); }
-
-#ifndef SDDC_WL
-#define SDDC_WL 0             // 1: wave-local forward FFT, 7 barriers per frame instead of 10 (measured neutral)
-#endif
-// Wave-local forward layout (SDDC_WL).  Wave w owns region [WL_WR w, WL_WR (w+1)) and the
-// four 256-point sub-FFTs k2 = 4w .. 4w+3, each in a padded slot of WL_RS elements.
-constexpr int WL_RS = 272, WL_WR = 4 * WL_RS, WL_LDS = 4 * WL_WR;
-// Z[k], k = k2 + 16 k1 + 256 k0, sits at WL_WR (k2 / 4) + zrow_low(k2, k1) + 64 k0: conflict-free
-// both for the pass-2 writes (16 lanes k1 = 0..15 per k2) and for the split's gathers
-// (32 consecutive k per read)
-__device__ __forceinline__ int zrow_low(int k2, int k1)
-{
-    return 32 * ((k2 >> 1) & 1) + ((k2 + k1) & 15) + 16 * (k1 & 1);
-}
-__device__ __forceinline__ int zpos(int k)   // k in [0, 4096)
-{
-    const int k2 = k & 15;
-    return WL_WR * (k2 >> 2) + zrow_low(k2, (k >> 4) & 15) + 64 * (k >> 8);
-}
-__device__ __forceinline__ void wave_sync()   // order LDS accesses across the lanes of one wave
-{
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 template <int DIR>
 __device__ __forceinline__ float2 tmul(float2 a, float2 w) { return DIR < 0 ? cmul(a, w) : cmulc(a, w); }
@@ -275,14 +242,11 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
     const float4 *__restrict__ pq, int tunebin, OutArgs oa, NcoArgs nco)
 {
     constexpr int N = HALF >> D;
-    static_assert(!(SDDC_WL && kDB), "the wave-local layout is single-buffered");
-    static_assert(!SDDC_WL || SDDC_PQ, "the wave-local layout reads Z through the (P, Q) split only");
-    constexpr int LDSN = SDDC_WL ? WL_LDS : HALF;
-    __shared__ __attribute__((aligned(16))) float2 lds[kDB ? 2 * LDSN : LDSN];
+    __shared__ __attribute__((aligned(16))) float2 lds[kDB ? 2 * HALF : HALF];
     // pass-1 twiddle tables, copied once per workgroup: [15][16] forward, [15][S] inverse
     constexpr int SQ = N >= 512 ? N / 256 : N / 16;
     __shared__ __attribute__((aligned(16))) float2 twl[15 * 16 + 15 * SQ];
-    float2 *w0 = lds, *w1 = kDB ? lds + LDSN : lds;   // this frame's pass buffers
+    float2 *w0 = lds, *w1 = kDB ? lds + HALF : lds;   // this frame's pass buffers
 
     const int tid = (int)threadIdx.x;
     const int G = (int)gridDim.x, w = (int)blockIdx.x;
@@ -338,92 +302,44 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
             if (SDDC_PREFETCH && f + 1 < f1) load_frame(in32, blk, k, x);   // prefetch the next frame
             DFT16<-1>(a, v);
         }
-        if constexpr (SDDC_WL) {
-            // ---- wave-local forward: scatter once, then both passes of each 256-point
-            //      sub-FFT inside one wave ----
-            TWREC16<-1>(v, fw1, fw4);                 // W_4096^{t k2}, applied by the writer
-            LOOP_SYNC();                              // every wave's previous LDS reads are done
-            WPRIO();
+        if constexpr (!kDB) LOOP_SYNC();   // the previous frame's last LDS reads are done
 #pragma unroll
-            for (int r = 0; r < 16; r++) LDS_WR w0[t + WL_RS * r] = v[r];   // k2 = r -> wave r / 4
-            LOOP_SYNC();
-            const int wv = t >> 6, j = (t >> 4) & 3;      // wave, sub-FFT k2 = 4 wv + j; x15 = n0
-            const int rb = WL_WR * wv + WL_RS * j;
-            // pass 1: DFT-16 over n1 of c = n0 + 16 n1, then W_256^{n0 k1}
-            {
-                float2 a[16];
+        for (int r = 0; r < 16; r++) LDS_WR w0[16 * t + (r ^ x15)] = v[r];          // swz(16t + r)
+        LOOP_SYNC();
+        // ---- forward pass 1 (R16, NS16): table twiddles W_256^{(t%16) r} ----
+        {
+            float2 a[16];
 #pragma unroll
-                for (int r = 0; r < 16; r++) a[r] = LDS_RD(w0[rb + x15 + 16 * r], v[r]);
-                DFT16<-1>(a, v);
+            for (int r = 0; r < 16; r++) a[r] = LDS_RD(w0[sT + NT * r], v[r]);
 #pragma unroll
-                for (int r = 1; r < 16; r++)
-                    v[r] = TW<-1>(v[r], (SDDC_FAKE & 2) ? make_float2(0.7f, 0.01f * (r + x15)) : twl[(r - 1) * 16 + x15]);
-            }
-            wave_sync();                              // this wave's pass-1 reads precede its writes
-            WPRIO();
-#pragma unroll
-            for (int r = 0; r < 16; r++) LDS_WR w0[rb + 17 * x15 + r] = v[r];
-            wave_sync();
-            // pass 2: DFT-16 over n0 for k1 = x15; Z[k2 + 16 k1 + 256 k0] with k0 = r
-            {
-                float2 a[16];
-#pragma unroll
-                for (int r = 0; r < 16; r++) a[r] = LDS_RD(w0[rb + x15 + 17 * r], v[r]);
-                DFT16<-1>(a, v);
-            }
-            wave_sync();
-            const int zb = WL_WR * wv + zrow_low(4 * wv + j, x15);
-            WPRIO();
-#pragma unroll
-            for (int r = 0; r < 16; r++) LDS_WR w0[zb + 64 * r] = v[r];   // = zpos(k)
-            LOOP_SYNC();
-        } else {
-            if constexpr (!kDB) LOOP_SYNC();   // the previous frame's last LDS reads are done
-            WPRIO();
-#pragma unroll
-            for (int r = 0; r < 16; r++) LDS_WR w0[16 * t + (r ^ x15)] = v[r];          // swz(16t + r)
-            LOOP_SYNC();
-            // ---- forward pass 1 (R16, NS16): table twiddles W_256^{(t%16) r} ----
-            {
-                float2 a[16];
-                PRIO(SDDC_PRIO);
-#pragma unroll
-                for (int r = 0; r < 16; r++) a[r] = LDS_RD(w0[sT + NT * r], v[r]);
-                PRIO(0);
-#pragma unroll
-                for (int r = 1; r < 16; r++)
-                    a[r] = TW<-1>(a[r], (SDDC_FAKE & 2) ? make_float2(0.7f, 0.01f * (r + x15)) : twl[(r - 1) * 16 + x15]);
-                DFT16<-1>(a, v);
-            }
-            if constexpr (!kDB) LOOP_SYNC();
-            {
-                const int b1 = (t >> 4) * 256;                                     // swz(b1 + x15 + 16 r)
-                WPRIO();
-#pragma unroll
-                for (int r = 0; r < 16; r++) LDS_WR w1[b1 + 16 * r + (x15 ^ r)] = v[r];
-            }
-            LOOP_SYNC();
-            // ---- forward pass 2 (R16, NS256): recurrence twiddles W_4096^{t r} ----
-            {
-                float2 a[16];
-                PRIO(SDDC_PRIO);
-#pragma unroll
-                for (int r = 0; r < 16; r++) a[r] = LDS_RD(w1[sT + NT * r], v[r]);
-                PRIO(0);
-                if constexpr (SDDC_TWTAB) {
-#pragma unroll
-                    for (int r = 1; r < 16; r++) a[r] = TW<-1>(a[r], ttf[(r - 1) * NT + t]);
-                } else {
-                    TWREC16<-1>(a, fw1, fw4);
-                }
-                DFT16<-1>(a, v);
-            }
-            if constexpr (!kDB) LOOP_SYNC();
-            WPRIO();
-#pragma unroll
-            for (int r = 0; r < 16; r++) LDS_WR w0[sT + NT * r] = v[r];   // Z, natural order
-            LOOP_SYNC();
+            for (int r = 1; r < 16; r++)
+                a[r] = TW<-1>(a[r], (SDDC_FAKE & 2) ? make_float2(0.7f, 0.01f * (r + x15)) : twl[(r - 1) * 16 + x15]);
+            DFT16<-1>(a, v);
         }
+        if constexpr (!kDB) LOOP_SYNC();
+        {
+            const int b1 = (t >> 4) * 256;                                     // swz(b1 + x15 + 16 r)
+#pragma unroll
+            for (int r = 0; r < 16; r++) LDS_WR w1[b1 + 16 * r + (x15 ^ r)] = v[r];
+        }
+        LOOP_SYNC();
+        // ---- forward pass 2 (R16, NS256): recurrence twiddles W_4096^{t r} ----
+        {
+            float2 a[16];
+#pragma unroll
+            for (int r = 0; r < 16; r++) a[r] = LDS_RD(w1[sT + NT * r], v[r]);
+            if constexpr (SDDC_TWTAB) {
+#pragma unroll
+                for (int r = 1; r < 16; r++) a[r] = TW<-1>(a[r], ttf[(r - 1) * NT + t]);
+            } else {
+                TWREC16<-1>(a, fw1, fw4);
+            }
+            DFT16<-1>(a, v);
+        }
+        if constexpr (!kDB) LOOP_SYNC();
+#pragma unroll
+        for (int r = 0; r < 16; r++) LDS_WR w0[sT + NT * r] = v[r];   // Z, natural order
+        LOOP_SYNC();
 
         if constexpr (N >= 512) {
             constexpr int R0 = N / 256;
@@ -435,11 +351,6 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
                 const int sc0 = swz(HALF - b0);              // mirror bin, same separability
                 const char *w0b = reinterpret_cast<const char *>(w0);
                 const unsigned sb0b = 8u * (unsigned)sb0, sc0b = 8u * (unsigned)sc0, tb16 = 16u * (unsigned)t;
-                // wave-local Z layout: bins b0 + 256 r share k & 255, so only the 64 k0 term moves
-                const int bk = b0 & (HALF - 1), bc = (HALF - b0) & (HALF - 1);
-                const unsigned zkl = 8u * (unsigned)(WL_WR * ((bk & 15) >> 2) + zrow_low(bk & 15, (bk >> 4) & 15));
-                const unsigned zcl = 8u * (unsigned)(WL_WR * ((bc & 15) >> 2) + zrow_low(bc & 15, (bc >> 4) & 15));
-                const unsigned zkh = 512u * (unsigned)(bk >> 8), zch = 512u * (unsigned)(bc >> 8);
                 const __amdgpu_buffer_rsrc_t rpq = buf_rsrc(pqz);
                 float2 a[R0];
 #pragma unroll
@@ -449,20 +360,6 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
                     const int bin = b0 + sh;
                     const int q = (r - (wrap ? N / NT : 0)) & 31;       // W_8192^{256 r - N wrap}
                     // branch-free: read a valid (wrapped) address; out-of-band bins have P = Q = 0
-                    if constexpr (SDDC_PQ && SDDC_WL) {
-                        const unsigned dh = 512u * (unsigned)(sh / NT);       // 64 k0 elements per 256 bins
-                        const float2 zk = LDS_RD(*reinterpret_cast<const float2 *>(
-                            w0b + zkl + ((zkh + dh) & (512u * 16u - 1u))), v[r]);
-                        const float2 zc = LDS_RD(*reinterpret_cast<const float2 *>(
-                            w0b + zcl + ((zch - dh) & (512u * 16u - 1u))), v[(r + 1) & 15]);
-                        float4 c;
-                        if constexpr (SDDC_FAKE & 1)
-                            c = make_float4(0.5f, 0.25f * r, 0.1f, 0.2f);
-                        else
-                            c = buf_load16(rpq, tb16, 16u * NT * r);
-                        a[r] = split_pq(zk, zc, c);
-                        continue;
-                    }
                     if constexpr (SDDC_PQ) {
                         // byte offsets: the wrap is one AND, the scale folds away
                         const float2 zk = LDS_RD(*reinterpret_cast<const float2 *>(
@@ -494,7 +391,6 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
             }
             if constexpr (!kDB) LOOP_SYNC();
             if constexpr (R0 == 16) {
-                WPRIO();
 #pragma unroll
                 for (int r = 0; r < 16; r++) LDS_WR w1[16 * t + (r ^ x15)] = u[r];
             } else {
@@ -508,10 +404,8 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
             if (act) {
                 float2 a[16];
                 if constexpr (NB == NT) {
-                    PRIO(SDDC_PRIO);
 #pragma unroll
                     for (int r = 0; r < 16; r++) a[r] = LDS_RD(w1[sT + NT * r], u[r]);
-                    PRIO(0);
                 } else {
 #pragma unroll
                     for (int r = 0; r < 16; r++) a[r] = w1[swz(t + NB * r)];
@@ -525,7 +419,6 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
             if (act) {
                 if constexpr (R0 == 16) {
                     const int b1 = (t >> 4) * 256;
-                    WPRIO();
 #pragma unroll
                     for (int r = 0; r < 16; r++) LDS_WR w0[b1 + 16 * r + (x15 ^ r)] = u[r];
                 } else {
@@ -539,10 +432,8 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
             if (act) {
                 float2 a[16];
                 if constexpr (NB == NT) {
-                    PRIO(SDDC_PRIO);
 #pragma unroll
                     for (int r = 0; r < 16; r++) a[r] = LDS_RD(w0[sT + NT * r], u[r]);
-                    PRIO(0);
                 } else {
 #pragma unroll
                     for (int r = 0; r < 16; r++) a[r] = w0[swz(t + NB * r)];
@@ -563,9 +454,7 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
             if (t < N) {
                 const int m = t;
                 const int bin = tunebin + m - (m >= N / 2 ? N : 0);
-                if constexpr (SDDC_PQ && SDDC_WL)
-                    tv = split_pq(w0[zpos(bin & (HALF - 1))], w0[zpos((HALF - bin) & (HALF - 1))], pqz[m]);
-                else if constexpr (SDDC_PQ)
+                if constexpr (SDDC_PQ)
                     tv = split_pq(w0[swz(bin & (HALF - 1))], w0[swz((HALF - bin) & (HALF - 1))], pqz[m]);
                 else
                     tv = split_bin(w0, bin, pst[bin & 8191], hs[m]);
