@@ -22,6 +22,7 @@ struct KernelTables {
     const float2 *rec_i[7] = {};       // [2][256]: W_N^{j}, W_N^{4j}        inverse pass 2 (N >= 512)
     const float2 *twt_f = nullptr;     // [15][256]: W_4096^{j r}   forward pass 2 twiddles (table form)
     const float2 *twt_i[7] = {};       // [15][N/16]: W_N^{j r}     inverse pass 2 twiddles (N >= 512)
+    const float2 *twf64 = nullptr;     // [64][64]: W_4096^{L q} at [q][L]  wave kernel F1 twiddles (d = 0)
 };
 
 // v1: one workgroup per frame (kept as a reference variant for A/B timing)
@@ -37,6 +38,14 @@ hipError_t launch_frames_persistent(const KernelTables &t, int d, const int16_t 
                                     int cs16, float cs16_scale, const float2 *nco_starts,
                                     const float2 *nco_trig, int device, hipStream_t s);
 hipError_t launch_build_split_filter(const KernelTables &t, int d, int tunebin, float4 *pq, hipStream_t s);
+
+// d = 0 wave kernel (ddc_wave.hip): one wave64 per frame, 64 points per lane.  pqW (4096
+// float4) and twI (4096 float2) are its per-tunebin tables, built by launch_build_wave_tables.
+hipError_t launch_build_wave_tables(const KernelTables &t, int tunebin, float4 *pqW, float2 *twI, hipStream_t s);
+hipError_t launch_frames_wave(const KernelTables &t, const int16_t *d_in, int nblk, void *d_out,
+                              const float4 *pqW, const float2 *twI, int tunebin, int lsb, int rand, int cs16,
+                              float cs16_scale, const float2 *nco_starts, const float2 *nco_trig, int device,
+                              hipStream_t s);
 
 int channels_per_group(int d, int nch);
 

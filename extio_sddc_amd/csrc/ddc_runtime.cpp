@@ -75,7 +75,8 @@ struct sddc_ddc {
     int device = 0;
     float gain = 0.f;
     int d = 0, lsb = 0, rand = 0, tunebin = SDDC_DDC_HALF_FFT / 4;   // ctor: mtunebin = halfFft/4
-    int variant = 0;                       // 0: persistent (v2), 1: one workgroup per frame (v1)
+    int variant = 0;                       // 0: persistent (v2); 1: one workgroup per frame (v1);
+                                           // 3: one wave per frame at d = 0 (ddc_wave.hip), persistent otherwise
     int out_fmt = SDDC_DDC_FMT_CF32;       // output stage format
     float cs16_scale = 1.f;
     sddc::KernelTables tables;
@@ -109,6 +110,9 @@ struct sddc_ddc {
     // changes; pq_used marks the last launch that read them (possibly on another stream)
     float4 *d_pq = nullptr;
     int pq_d = -1, pq_tb = -1;
+    // the d = 0 wave kernel's per-tunebin tables: pqW (4096 float4) then twI (4096 float2)
+    float4 *d_wave = nullptr;
+    int wave_tb = -1;
     hipEvent_t pq_used = nullptr;
     hipStream_t pq_stream = nullptr;
 
@@ -206,6 +210,9 @@ int sddc_ddc_create(float gain, int device, sddc_ddc_t **out)
         host[o_recf + j] = W(j, 4096);
         host[o_recf + 256 + j] = W(4.0 * j, 4096);
     }
+    const size_t o_twf64 = put(64 * 64);   // wave kernel F1 twiddles W_4096^{L q} at [q][L]
+    for (int q = 0; q < 64; q++)
+        for (int L = 0; L < 64; L++) host[o_twf64 + 64 * q + L] = W((double)((L * q) & 4095), 4096);
     const size_t o_twtf = put(15 * 256);
     for (int r = 1; r < 16; r++)
         for (int j = 0; j < 256; j++) host[o_twtf + (r - 1) * 256 + j] = W((double)j * r, 4096);
@@ -243,6 +250,7 @@ int sddc_ddc_create(float gain, int device, sddc_ddc_t **out)
     if (e == hipSuccess) e = hipMemcpy(h->d_tables, host.data(), ntab * sizeof(float2), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipMalloc(&h->d_pq, SDDC_DDC_HALF_FFT * sizeof(float4));
+    if (e == hipSuccess) e = hipMalloc(&h->d_wave, 4096 * (sizeof(float4) + sizeof(float2)));
     if (e == hipSuccess) e = hipEventCreateWithFlags(&h->pq_used, hipEventDisableTiming);
     if (e != hipSuccess) {
         sddc_ddc_destroy(h);
@@ -254,6 +262,7 @@ int sddc_ddc_create(float gain, int device, sddc_ddc_t **out)
     h->tables.tw_p1 = T + o_p1;
     h->tables.rec_f = T + o_recf;
     h->tables.twt_f = T + o_twtf;
+    h->tables.twf64 = T + o_twf64;
     for (int d = 0; d < SDDC_DDC_NDEC; d++) {
         h->tables.hsel[d] = T + o_hsel[d];
         h->tables.tw_q1[d] = T + o_q1[d];
@@ -285,6 +294,7 @@ int sddc_ddc_destroy(sddc_ddc_t *h)
         if (h->d_tunebins) (void)hipFree(h->d_tunebins);
         if (h->d_windows) (void)hipFree(h->d_windows);
         if (h->d_pq) (void)hipFree(h->d_pq);
+        if (h->d_wave) (void)hipFree(h->d_wave);
         if (h->pq_used) (void)hipEventDestroy(h->pq_used);
         for (int i = 0; i < sddc_ddc::kNcoSlots; i++) {
             if (h->h_nco[i]) (void)hipHostFree(h->h_nco[i]);
@@ -408,6 +418,26 @@ static hipError_t launch_single(sddc_ddc_t *h, const int16_t *d_in, int nblk, vo
         hipError_t e = stage_nco(h, nblk, s);
         if (e != hipSuccess) return e;
     }
+    if (h->d == 0 && h->variant == 3) {
+        // wave kernel (ddc_wave.hip): its (P, Q) and inverse twiddles in lane layout
+        float4 *pqW = h->d_wave;
+        float2 *twI = reinterpret_cast<float2 *>(h->d_wave + 4096);
+        if (h->wave_tb != h->tunebin) {
+            if (h->pq_stream && h->pq_stream != s) {   // a launch on another stream may still read them
+                hipError_t e = hipStreamWaitEvent(s, h->pq_used, 0);
+                if (e != hipSuccess) return e;
+            }
+            hipError_t e = sddc::launch_build_wave_tables(h->tables, h->tunebin, pqW, twI, s);
+            if (e != hipSuccess) return e;
+            h->wave_tb = h->tunebin;
+        }
+        hipError_t e = sddc::launch_frames_wave(
+            h->tables, d_in, nblk, d_out, pqW, twI, h->tunebin, h->lsb, h->rand, h->out_fmt == SDDC_DDC_FMT_CS16,
+            h->cs16_scale, nco ? h->d_nco + sddc::FineTune::kTable : nullptr, nco ? h->d_nco : nullptr, h->device, s);
+        if (e != hipSuccess) return e;
+        h->pq_stream = s;
+        return hipEventRecord(h->pq_used, s);
+    }
     if (h->pq_d != h->d || h->pq_tb != h->tunebin) {
         if (h->pq_stream && h->pq_stream != s) {   // a launch on another stream may still read d_pq
             hipError_t e = hipStreamWaitEvent(s, h->pq_used, 0);
@@ -455,7 +485,7 @@ int sddc_ddc_set_fine_tune(sddc_ddc_t *h, float relative_freq)
 /* internal (not in include/sddc_ddc.h): kernel variant for A/B timing, see sddc_ddc_internal.h */
 int sddc_ddc_internal_set_variant(sddc_ddc_t *h, int variant)
 {
-    if (!h || variant < 0 || variant > 1) return fail(SDDC_ERR_ARG, "bad variant");
+    if (!h || variant < 0 || variant > 3 || variant == 2) return fail(SDDC_ERR_ARG, "bad variant");
     h->variant = variant;
     return SDDC_OK;
 }
@@ -502,7 +532,7 @@ int sddc_ddc_process_channels_device(sddc_ddc_t *h, const int16_t *d_in, int nbl
     HIP_TRY(g.err);
     std::lock_guard<std::mutex> lk(h->mu);
     hipStream_t s = (hipStream_t)hip_stream;
-    const bool v2 = h->d >= 4 && h->variant == 0;
+    const bool v2 = h->d >= 4 && h->variant != 1;
     const bool changed = h->tunebins_cached.size() != (size_t)nch ||
                          !std::equal(h->tunebins_cached.begin(), h->tunebins_cached.end(), tunebins);
     if (changed || (v2 && h->windows_d != h->d && h->windows_d != -2 - 8 * h->d)) {
