@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--tunebin", type=int, default=1024)
     ap.add_argument("--channels", type=int, default=0, help="time process_channels_device with tune bins 4c")
+    ap.add_argument("--variant", type=int, default=0, help="single-channel kernel (sddc_ddc_internal.h)")
     args = ap.parse_args()
 
     import torch
@@ -43,6 +44,9 @@ def main():
         rc = L.sddc_ddc_create(1.0, 0, ctypes.byref(h))
         assert rc == 0, L.sddc_ddc_last_error()
         L.sddc_ddc_set_tunebin(h, args.tunebin)
+        if args.variant:
+            L.sddc_ddc_internal_set_variant.argtypes = [ctypes.c_void_p, ctypes.c_int]
+            assert L.sddc_ddc_internal_set_variant(h, args.variant) == 0
         libs.append(L)
         handles.append(h)
     nblk = args.nblk
