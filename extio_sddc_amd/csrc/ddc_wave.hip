@@ -41,6 +41,11 @@ constexpr int BLOCK = 65536;
 constexpr int FRAMES = 11;
 constexpr int LDS_STRIDE = 33;   // padded row: writes and reads are base + immediate, conflict-free
 
+#ifndef SDDC_WV_FAKE
+#define SDDC_WV_FAKE 0           // timing-only builds: 1 = no table loads, 2 = no LDS exchange reads,
+                                 // 4 = no IQ stores, 8 = no input (DMA + LDS reads)
+#endif
+
 #ifndef SDDC_WV_WAVES
 #define SDDC_WV_WAVES 2          // __launch_bounds__ min waves per SIMD (<= 256 VGPRs)
 #endif
@@ -187,7 +192,8 @@ __device__ __forceinline__ void load_frame_lds(const int *__restrict__ in32, int
 __device__ __forceinline__ void tw_load(float2 (&w)[8], __amdgpu_buffer_rsrc_t r, unsigned l8, int g)
 {
 #pragma unroll
-    for (int i = (g == 0); i < 8; i++) w[i] = buf_load8(r, l8, 512u * (8 * g + i));
+    for (int i = (g == 0); i < 8; i++)
+        w[i] = (SDDC_WV_FAKE & 1) ? make_float2(__uint_as_float(0x3f000000u | l8), 0.25f) : buf_load8(r, l8, 512u * (8 * g + i));
 }
 __device__ __forceinline__ void tw_pre(float2 (&w)[3][8], __amdgpu_buffer_rsrc_t r, unsigned l8)
 {
@@ -208,6 +214,11 @@ __device__ __forceinline__ void tw_apply(float2 *R, float2 (&w)[3][8], __amdgpu_
 // (P, Q) of split quad j: S registers j, 31-j and D registers j, 31-j
 __device__ __forceinline__ void pq_load(float4 (&c)[4], __amdgpu_buffer_rsrc_t r, unsigned l16, int j)
 {
+    if constexpr (SDDC_WV_FAKE & 1) {
+        const float f = __uint_as_float(0x3f000000u | l16);
+        c[0] = c[1] = c[2] = c[3] = make_float4(f, 0.25f, 0.5f, f);
+        return;
+    }
     c[0] = buf_load16(r, l16, 1024u * j);
     c[1] = buf_load16(r, l16, 1024u * (31 - j));
     c[2] = buf_load16(r, l16, 1024u * (32 + j));
@@ -269,7 +280,7 @@ __global__ __launch_bounds__(64, SDDC_WV_WAVES) void r2iq_wave_kernel(
             const int *xi = reinterpret_cast<const int *>(xl) + lane;
 #pragma unroll
             for (int r = 0; r < 64; r++) {
-                const int v = xi[64 * r];
+                const int v = (SDDC_WV_FAKE & 8) ? (int)(lane * 2654435761u + r * 40503u + f) : xi[64 * r];
                 a[r] = make_float2(derand_w<RAND>((int)(short)(v & 0xffff)), derand_w<RAND>(v >> 16));
             }
             if (++k == FRAMES) {
@@ -288,13 +299,13 @@ __global__ __launch_bounds__(64, SDDC_WV_WAVES) void r2iq_wave_kernel(
         for (int q = 0; q < 32; q++) xl[wF + q] = R[q];
         WAVE_SYNC();
 #pragma unroll
-        for (int i = 0; i < 32; i++) R[i] = xl[rA + LDS_STRIDE * i];
+        for (int i = 0; i < 32; i++) R[i] = (SDDC_WV_FAKE & 2) ? R[i] : xl[rA + LDS_STRIDE * i];
         WAVE_SYNC();
 #pragma unroll
         for (int q = 0; q < 32; q++) xl[wF + q] = R[32 + q];
         WAVE_SYNC();
 #pragma unroll
-        for (int i = 0; i < 32; i++) R[32 + i] = xl[rB + LDS_STRIDE * i];
+        for (int i = 0; i < 32; i++) R[32 + i] = (SDDC_WV_FAKE & 2) ? R[32 + i] : xl[rB + LDS_STRIDE * i];
         WAVE_SYNC();
 
         // ---- F2: full column per lane, DIF on the row's top bit ----
@@ -360,13 +371,13 @@ __global__ __launch_bounds__(64, SDDC_WV_WAVES) void r2iq_wave_kernel(
         for (int n = 0; n < 32; n++) xl[wI + n] = R[n];
         WAVE_SYNC();
 #pragma unroll
-        for (int i = 0; i < 32; i++) R[i] = xl[rA + LDS_STRIDE * i];
+        for (int i = 0; i < 32; i++) R[i] = (SDDC_WV_FAKE & 2) ? R[i] : xl[rA + LDS_STRIDE * i];
         WAVE_SYNC();
 #pragma unroll
         for (int n = 0; n < 32; n++) xl[wI + n] = R[32 + n];
         WAVE_SYNC();
 #pragma unroll
-        for (int i = 0; i < 32; i++) R[32 + i] = xl[rA + LDS_STRIDE * i];
+        for (int i = 0; i < 32; i++) R[32 + i] = (SDDC_WV_FAKE & 2) ? R[32 + i] : xl[rA + LDS_STRIDE * i];
         WAVE_SYNC();
 
         // ---- I2: lane l holds column n_lo = l; DIF on the top bit of m_lo ----
@@ -382,7 +393,7 @@ __global__ __launch_bounds__(64, SDDC_WV_WAVES) void r2iq_wave_kernel(
             // the exchange buffer is free again: stage the next frame (the swaps above consumed
             // every read of it); the last frame of the range stages itself again, unused
             __builtin_amdgcn_wave_barrier();
-            load_frame_lds(in32, f + 1 < f1 ? blk : blk_c, f + 1 < f1 ? k : k_c, xl);
+            if constexpr (!(SDDC_WV_FAKE & 8)) load_frame_lds(in32, f + 1 < f1 ? blk : blk_c, f + 1 < f1 ? k : k_c, xl);
             dft32<+1>(s, Ye);   // y[l + 64 * 2j]
             dft32<+1>(d, Yo);   // y[l + 64 * (2j + 1)]
         }
@@ -399,7 +410,7 @@ __global__ __launch_bounds__(64, SDDC_WV_WAVES) void r2iq_wave_kernel(
                 const int nhi = 2 * j + par;
                 float2 v = flip(par ? Yo[j] : Ye[j], oa.lsbmask);
                 if constexpr (NCO) v = nco_mix(v, nco, fbase + lane + 64 * nhi);
-                store_iq<CS16>(v, ro, (unsigned)lane, (unsigned)(64 * nhi), oa);
+                if (!(SDDC_WV_FAKE & 4) || v.x == 1.2345e30f) store_iq<CS16>(v, ro, (unsigned)lane, (unsigned)(64 * nhi), oa);
             }
         }
     }
@@ -455,6 +466,9 @@ hipError_t launch_w(const float2 *twF, const float4 *pqW, const float2 *twI, con
         if (e != hipSuccess) return e;
         g_wcus = cus;
         occ = nb > 0 ? nb : 1;
+#ifdef SDDC_WV_OCC
+        occ = occ < SDDC_WV_OCC ? occ : SDDC_WV_OCC;   // A/B builds: resident waves per CU
+#endif
     }
     const int nframes = nblk * FRAMES;
     int grid = g_wcus * occ;
