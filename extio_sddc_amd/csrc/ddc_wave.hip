@@ -43,95 +43,19 @@ constexpr int LDS_STRIDE = 33;   // padded row: writes and reads are base + imme
 
 #ifndef SDDC_WV_FAKE
 #define SDDC_WV_FAKE 0           // timing-only builds: 1 = no table loads, 2 = no LDS exchange reads,
-                                 // 4 = no IQ stores, 8 = no input (DMA + LDS reads)
+                                 // 4 = no IQ stores, 8 = no input (DMA + LDS reads),
+                                 // 16 = no v_permlane32_swap (swaps and rotations are identities),
+                                 // 32 = no lane-0/32 selects
 #endif
 
 #ifndef SDDC_WV_WAVES
 #define SDDC_WV_WAVES 2          // __launch_bounds__ min waves per SIMD (<= 256 VGPRs)
 #endif
 
-// cos / sin(2 pi m / 64)
-__device__ constexpr float kC64[64] = {
-    1.0f, 0.99518472667219693f, 0.98078528040323043f, 0.95694033573220882f, 0.92387953251128674f,
-    0.88192126434835505f, 0.83146961230254524f, 0.77301045336273699f, 0.70710678118654757f,
-    0.63439328416364549f, 0.55557023301960218f, 0.47139673682599764f, 0.38268343236508978f,
-    0.29028467725446233f, 0.19509032201612825f, 0.098017140329560604f, 0.0f, -0.098017140329560604f,
-    -0.19509032201612825f, -0.29028467725446233f, -0.38268343236508978f, -0.47139673682599764f,
-    -0.55557023301960218f, -0.63439328416364549f, -0.70710678118654757f, -0.77301045336273699f,
-    -0.83146961230254524f, -0.88192126434835505f, -0.92387953251128674f, -0.95694033573220882f,
-    -0.98078528040323043f, -0.99518472667219693f, -1.0f, -0.99518472667219693f, -0.98078528040323043f,
-    -0.95694033573220882f, -0.92387953251128674f, -0.88192126434835505f, -0.83146961230254524f,
-    -0.77301045336273699f, -0.70710678118654757f, -0.63439328416364549f, -0.55557023301960218f,
-    -0.47139673682599764f, -0.38268343236508978f, -0.29028467725446233f, -0.19509032201612825f,
-    -0.098017140329560604f, 0.0f, 0.098017140329560604f, 0.19509032201612825f, 0.29028467725446233f,
-    0.38268343236508978f, 0.47139673682599764f, 0.55557023301960218f, 0.63439328416364549f,
-    0.70710678118654757f, 0.77301045336273699f, 0.83146961230254524f, 0.88192126434835505f,
-    0.92387953251128674f, 0.95694033573220882f, 0.98078528040323043f, 0.99518472667219693f};
-
-// a * e^{DIR 2 pi i m / 64}; m is a constant after unrolling, so the special cases fold
-template <int DIR>
-__device__ __forceinline__ float2 tw64(float2 a, int m)
-{
-    m &= 63;
-    if (m == 0) return a;
-    if (m == 16) return mulj<DIR>(a);
-    if (m == 32) return make_float2(-a.x, -a.y);
-    if (m == 48) return mulj<-DIR>(a);
-    const float c = kC64[m], s = DIR * kC64[(m + 48) & 63];   // sin(x) = cos(x - pi/2)
-    return make_float2(c * a.x - s * a.y, c * a.y + s * a.x);
-}
-
-// DFT-32, natural order in and out: n = 4 n1 + n2, k = k1 + 8 k2
-template <int DIR>
-__device__ __forceinline__ void dft32(const float2 *x, float2 *o)
-{
-    float2 b[4][8];
-#pragma unroll
-    for (int n2 = 0; n2 < 4; n2++) {
-        float2 v[8];
-#pragma unroll
-        for (int n1 = 0; n1 < 8; n1++) v[n1] = x[4 * n1 + n2];
-        dft8<DIR>(v, b[n2]);
-    }
-#pragma unroll
-    for (int n2 = 1; n2 < 4; n2++)
-#pragma unroll
-        for (int k1 = 1; k1 < 8; k1++) b[n2][k1] = tw64<DIR>(b[n2][k1], 2 * n2 * k1);
-#pragma unroll
-    for (int k1 = 0; k1 < 8; k1++)
-        dft4<DIR>(b[0][k1], b[1][k1], b[2][k1], b[3][k1], o[k1], o[k1 + 8], o[k1 + 16], o[k1 + 24]);
-}
-
-// DFT-64, natural order in and out: n = 8 n1 + n2, k = k1 + 8 k2
-template <int DIR>
-__device__ __forceinline__ void dft64(const float2 *x, float2 *o)
-{
-    float2 b[8][8];
-#pragma unroll
-    for (int n2 = 0; n2 < 8; n2++) {
-        float2 v[8];
-#pragma unroll
-        for (int n1 = 0; n1 < 8; n1++) v[n1] = x[8 * n1 + n2];
-        dft8<DIR>(v, b[n2]);
-    }
-#pragma unroll
-    for (int n2 = 1; n2 < 8; n2++)
-#pragma unroll
-        for (int k1 = 1; k1 < 8; k1++) b[n2][k1] = tw64<DIR>(b[n2][k1], n2 * k1);
-#pragma unroll
-    for (int k1 = 0; k1 < 8; k1++) {
-        float2 v[8], w[8];
-#pragma unroll
-        for (int n2 = 0; n2 < 8; n2++) v[n2] = b[n2][k1];
-        dft8<DIR>(v, w);
-#pragma unroll
-        for (int k2 = 0; k2 < 8; k2++) o[k1 + 8 * k2] = w[k2];
-    }
-}
-
 // (a, b) <- v_permlane32_swap(a, b): lanes 32-63 of a <-> lanes 0-31 of b, both components
 __device__ __forceinline__ void swap32(float2 &a, float2 &b)
 {
+    if constexpr (SDDC_WV_FAKE & 16) return;
     const auto x = __builtin_amdgcn_permlane32_swap(__float_as_uint(a.x), __float_as_uint(b.x), false, false);
     const auto y = __builtin_amdgcn_permlane32_swap(__float_as_uint(a.y), __float_as_uint(b.y), false, false);
     a = make_float2(__uint_as_float(x[0]), __uint_as_float(y[0]));
@@ -147,8 +71,13 @@ __device__ __forceinline__ void rotate32_except(float2 *d, bool keep)
         float2 p0 = d[a], p1 = d[a + 1];
         swap32(p0, p1);   // p0 = [d0 lo | d1 lo], p1 = [d0 hi | d1 hi]
         swap32(p1, p0);   // p1 = [d0 hi | d0 lo] = rot d0, p0 = [d1 hi | d1 lo] = rot d1
-        d[a] = keep ? d[a] : p1;
-        d[a + 1] = keep ? d[a + 1] : p0;
+        if constexpr (SDDC_WV_FAKE & 32) {
+            d[a] = p1;
+            d[a + 1] = p0;
+        } else {
+            d[a] = keep ? d[a] : p1;
+            d[a + 1] = keep ? d[a + 1] : p0;
+        }
     }
 }
 
@@ -164,6 +93,50 @@ __device__ __forceinline__ void rotate32_except(float2 *d, bool keep)
         __builtin_amdgcn_wave_barrier();                           \
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");     \
     } while (0)
+
+#ifndef SDDC_WV_LDSX
+#define SDDC_WV_LDSX 1           // 0: every half-wave exchange by v_permlane32_swap; 1: the two
+                                 // rotations through LDS; 2: the two half-swaps through LDS as well
+#endif
+
+// The half-wave exchanges through the (then idle) LDS exchange buffer instead of
+// v_permlane32_swap: a swap issues at ~7.5 cycles per SIMD and does not overlap across waves
+// (profiles/r01/wave/microbench_permlane.txt), while these 32 + 32 LDS operations per set use
+// the otherwise lightly loaded LDS pipe.  Row stride LDS_STRIDE keeps them conflict-free.
+//   swap_halves_lds(lo, hi) == swap32(lo[i], hi[i]) for every i: lanes < 32 receive lane+32's
+//   lo[] into hi[], lanes >= 32 receive lane-32's hi[] into lo[] (exec-masked halves).
+__device__ __forceinline__ void swap_halves_lds(float2 *lo, float2 *hi, float2 *xl, int lane)
+{
+    const int w = LDS_STRIDE * lane, r = LDS_STRIDE * (lane ^ 32);
+    if (lane < 32) {
+#pragma unroll
+        for (int i = 0; i < 32; i++) xl[w + i] = hi[i];
+    } else {
+#pragma unroll
+        for (int i = 0; i < 32; i++) xl[w + i] = lo[i];
+    }
+    WAVE_SYNC();
+    if (lane < 32) {
+#pragma unroll
+        for (int i = 0; i < 32; i++) hi[i] = xl[r + i];
+    } else {
+#pragma unroll
+        for (int i = 0; i < 32; i++) lo[i] = xl[r + i];
+    }
+    WAVE_SYNC();
+}
+//   rotate_lds(d, keep) == rotate32_except(d, keep): every lane reads lane^32's d[], the keep
+//   lanes (0 and 32) read their own, so no selects
+__device__ __forceinline__ void rotate_lds(float2 *d, bool keep, float2 *xl, int lane)
+{
+    const int w = LDS_STRIDE * lane, r = LDS_STRIDE * (keep ? lane : (lane ^ 32));
+#pragma unroll
+    for (int i = 0; i < 32; i++) xl[w + i] = d[i];
+    WAVE_SYNC();
+#pragma unroll
+    for (int i = 0; i < 32; i++) d[i] = xl[r + i];
+    WAVE_SYNC();
+}
 
 template <bool RAND>
 __device__ __forceinline__ float derand_w(int v)
@@ -313,9 +286,10 @@ __global__ __launch_bounds__(64, SDDC_WV_WAVES) void r2iq_wave_kernel(
         float4 cq[3][4];   // (P, Q) of three quads: loads run two quads ahead
         {
             float2 s[32], d[32];
+            if constexpr (SDDC_WV_LDSX >= 2) swap_halves_lds(R, R + 32, xl, lane);
 #pragma unroll
             for (int i = 0; i < 32; i++) {
-                swap32(R[i], R[32 + i]);
+                if constexpr (SDDC_WV_LDSX < 2) swap32(R[i], R[32 + i]);
                 s[i] = cadd(R[i], R[32 + i]);
                 d[i] = tw64<-1>(csub(R[i], R[32 + i]), i);
             }
@@ -325,7 +299,8 @@ __global__ __launch_bounds__(64, SDDC_WV_WAVES) void r2iq_wave_kernel(
             dft32<-1>(s, S);   // Z[c + 64 * 2j]
             dft32<-1>(d, D);   // Z[c + 64 * (2j + 1)]
         }
-        rotate32_except(D, keep);
+        if constexpr (SDDC_WV_LDSX) rotate_lds(D, keep, xl, lane);
+        else rotate32_except(D, keep);
 
         // ---- split x filter (T = Z_k P + conj(Z_-k) Q), mirrors in the same lane ----
         // Generic lanes pair S[j] with D[31-j]; lane 0 (column 0) pairs S[j] with S[32-j] and
@@ -338,10 +313,11 @@ __global__ __launch_bounds__(64, SDDC_WV_WAVES) void r2iq_wave_kernel(
             const int jb = 31 - j;
             if (j + 2 < 16) pq_load(cq[(j + 2) % 3], rpq, l16, j + 2);
             const float4 *c = cq[j % 3];
-            const float2 ms0 = lane0 ? S[(32 - j) & 31] : D[jb];
-            const float2 ms1 = lane0 ? S[(32 - jb) & 31] : D[j];
-            const float2 md0 = lane0 ? D[jb] : S[jb];
-            const float2 md1 = lane0 ? D[j] : S[j];
+            const bool l0 = (SDDC_WV_FAKE & 32) ? false : lane0;
+            const float2 ms0 = l0 ? S[(32 - j) & 31] : D[jb];
+            const float2 ms1 = l0 ? S[(32 - jb) & 31] : D[j];
+            const float2 md0 = l0 ? D[jb] : S[jb];
+            const float2 md1 = l0 ? D[j] : S[j];
             TS[j] = split_w(S[j], ms0, c[0]);
             TS[jb] = split_w(S[jb], ms1, c[1]);
             TD[j] = split_w(D[j], md0, c[2]);
@@ -357,7 +333,8 @@ __global__ __launch_bounds__(64, SDDC_WV_WAVES) void r2iq_wave_kernel(
             dft32<+1>(TD, O);
 #pragma unroll
             for (int n = 1; n < 32; n++) O[n] = tw64<+1>(O[n], n);
-            rotate32_except(O, keep);
+            if constexpr (SDDC_WV_LDSX) rotate_lds(O, keep, xl, lane);
+            else rotate32_except(O, keep);
 #pragma unroll
             for (int n = 0; n < 32; n++) {
                 R[n] = cadd(E[n], O[n]);
@@ -384,9 +361,10 @@ __global__ __launch_bounds__(64, SDDC_WV_WAVES) void r2iq_wave_kernel(
         float2 Ye[32], Yo[32];
         {
             float2 s[32], d[32];
+            if constexpr (SDDC_WV_LDSX >= 2) swap_halves_lds(R, R + 32, xl, lane);
 #pragma unroll
             for (int i = 0; i < 32; i++) {
-                swap32(R[i], R[32 + i]);
+                if constexpr (SDDC_WV_LDSX < 2) swap32(R[i], R[32 + i]);
                 s[i] = cadd(R[i], R[32 + i]);
                 d[i] = tw64<+1>(csub(R[i], R[32 + i]), i);
             }

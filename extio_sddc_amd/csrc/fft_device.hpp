@@ -141,6 +141,88 @@ __device__ __forceinline__ void dft(const float2 *v, float2 *o)
 }
 
 // ---------------------------------------------------------------------------
+// DFT-32 and DFT-64 in registers (the one-wave-per-frame kernel, ddc_wave.hip)
+// ---------------------------------------------------------------------------
+// cos / sin(2 pi m / 64)
+__device__ constexpr float kC64[64] = {
+    1.0f, 0.99518472667219693f, 0.98078528040323043f, 0.95694033573220882f, 0.92387953251128674f,
+    0.88192126434835505f, 0.83146961230254524f, 0.77301045336273699f, 0.70710678118654757f,
+    0.63439328416364549f, 0.55557023301960218f, 0.47139673682599764f, 0.38268343236508978f,
+    0.29028467725446233f, 0.19509032201612825f, 0.098017140329560604f, 0.0f, -0.098017140329560604f,
+    -0.19509032201612825f, -0.29028467725446233f, -0.38268343236508978f, -0.47139673682599764f,
+    -0.55557023301960218f, -0.63439328416364549f, -0.70710678118654757f, -0.77301045336273699f,
+    -0.83146961230254524f, -0.88192126434835505f, -0.92387953251128674f, -0.95694033573220882f,
+    -0.98078528040323043f, -0.99518472667219693f, -1.0f, -0.99518472667219693f, -0.98078528040323043f,
+    -0.95694033573220882f, -0.92387953251128674f, -0.88192126434835505f, -0.83146961230254524f,
+    -0.77301045336273699f, -0.70710678118654757f, -0.63439328416364549f, -0.55557023301960218f,
+    -0.47139673682599764f, -0.38268343236508978f, -0.29028467725446233f, -0.19509032201612825f,
+    -0.098017140329560604f, 0.0f, 0.098017140329560604f, 0.19509032201612825f, 0.29028467725446233f,
+    0.38268343236508978f, 0.47139673682599764f, 0.55557023301960218f, 0.63439328416364549f,
+    0.70710678118654757f, 0.77301045336273699f, 0.83146961230254524f, 0.88192126434835505f,
+    0.92387953251128674f, 0.95694033573220882f, 0.98078528040323043f, 0.99518472667219693f};
+
+// a * e^{DIR 2 pi i m / 64}; m is a constant after unrolling, so the special cases fold
+template <int DIR>
+__device__ __forceinline__ float2 tw64(float2 a, int m)
+{
+    m &= 63;
+    if (m == 0) return a;
+    if (m == 16) return mulj<DIR>(a);
+    if (m == 32) return make_float2(-a.x, -a.y);
+    if (m == 48) return mulj<-DIR>(a);
+    const float c = kC64[m], s = DIR * kC64[(m + 48) & 63];   // sin(x) = cos(x - pi/2)
+    return make_float2(c * a.x - s * a.y, c * a.y + s * a.x);
+}
+
+// DFT-32, natural order in and out: n = 4 n1 + n2, k = k1 + 8 k2
+template <int DIR>
+__device__ __forceinline__ void dft32(const float2 *x, float2 *o)
+{
+    float2 b[4][8];
+#pragma unroll
+    for (int n2 = 0; n2 < 4; n2++) {
+        float2 v[8];
+#pragma unroll
+        for (int n1 = 0; n1 < 8; n1++) v[n1] = x[4 * n1 + n2];
+        dft8<DIR>(v, b[n2]);
+    }
+#pragma unroll
+    for (int n2 = 1; n2 < 4; n2++)
+#pragma unroll
+        for (int k1 = 1; k1 < 8; k1++) b[n2][k1] = tw64<DIR>(b[n2][k1], 2 * n2 * k1);
+#pragma unroll
+    for (int k1 = 0; k1 < 8; k1++)
+        dft4<DIR>(b[0][k1], b[1][k1], b[2][k1], b[3][k1], o[k1], o[k1 + 8], o[k1 + 16], o[k1 + 24]);
+}
+
+// DFT-64, natural order in and out: n = 8 n1 + n2, k = k1 + 8 k2
+template <int DIR>
+__device__ __forceinline__ void dft64(const float2 *x, float2 *o)
+{
+    float2 b[8][8];
+#pragma unroll
+    for (int n2 = 0; n2 < 8; n2++) {
+        float2 v[8];
+#pragma unroll
+        for (int n1 = 0; n1 < 8; n1++) v[n1] = x[8 * n1 + n2];
+        dft8<DIR>(v, b[n2]);
+    }
+#pragma unroll
+    for (int n2 = 1; n2 < 8; n2++)
+#pragma unroll
+        for (int k1 = 1; k1 < 8; k1++) b[n2][k1] = tw64<DIR>(b[n2][k1], n2 * k1);
+#pragma unroll
+    for (int k1 = 0; k1 < 8; k1++) {
+        float2 v[8], w[8];
+#pragma unroll
+        for (int n2 = 0; n2 < 8; n2++) v[n2] = b[n2][k1];
+        dft8<DIR>(v, w);
+#pragma unroll
+        for (int k2 = 0; k2 < 8; k2++) o[k1 + 8 * k2] = w[k2];
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Packed-FP32 variants (gfx950 v_pk_{add,mul,fma}_f32 on (re, im) register pairs).
 // The ±i rotations and the operand swaps of a complex product ride on the VOP3P
 // op_sel / op_sel_hi / neg_lo / neg_hi source modifiers, so a butterfly is one
