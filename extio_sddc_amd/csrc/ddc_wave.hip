@@ -96,35 +96,15 @@ __device__ __forceinline__ void rotate32_except(float2 *d, bool keep)
 
 #ifndef SDDC_WV_LDSX
 #define SDDC_WV_LDSX 1           // 0: every half-wave exchange by v_permlane32_swap; 1: the two
-                                 // rotations through LDS; 2: the two half-swaps through LDS as well
+                                 // rotations through LDS (the half-swaps through LDS as well needed
+                                 // exec-masked halves, which hipcc if-converted and spilled: 6x
+                                 // slower; removed, in git history)
 #endif
 
-// The half-wave exchanges through the (then idle) LDS exchange buffer instead of
+// The two 32-lane rotations through the (then idle) LDS exchange buffer instead of
 // v_permlane32_swap: a swap issues at ~7.5 cycles per SIMD and does not overlap across waves
 // (profiles/r01/wave/microbench_permlane.txt), while these 32 + 32 LDS operations per set use
 // the otherwise lightly loaded LDS pipe.  Row stride LDS_STRIDE keeps them conflict-free.
-//   swap_halves_lds(lo, hi) == swap32(lo[i], hi[i]) for every i: lanes < 32 receive lane+32's
-//   lo[] into hi[], lanes >= 32 receive lane-32's hi[] into lo[] (exec-masked halves).
-__device__ __forceinline__ void swap_halves_lds(float2 *lo, float2 *hi, float2 *xl, int lane)
-{
-    const int w = LDS_STRIDE * lane, r = LDS_STRIDE * (lane ^ 32);
-    if (lane < 32) {
-#pragma unroll
-        for (int i = 0; i < 32; i++) xl[w + i] = hi[i];
-    } else {
-#pragma unroll
-        for (int i = 0; i < 32; i++) xl[w + i] = lo[i];
-    }
-    WAVE_SYNC();
-    if (lane < 32) {
-#pragma unroll
-        for (int i = 0; i < 32; i++) hi[i] = xl[r + i];
-    } else {
-#pragma unroll
-        for (int i = 0; i < 32; i++) lo[i] = xl[r + i];
-    }
-    WAVE_SYNC();
-}
 //   rotate_lds(d, keep) == rotate32_except(d, keep): every lane reads lane^32's d[], the keep
 //   lanes (0 and 32) read their own, so no selects
 __device__ __forceinline__ void rotate_lds(float2 *d, bool keep, float2 *xl, int lane)
@@ -286,10 +266,9 @@ __global__ __launch_bounds__(64, SDDC_WV_WAVES) void r2iq_wave_kernel(
         float4 cq[3][4];   // (P, Q) of three quads: loads run two quads ahead
         {
             float2 s[32], d[32];
-            if constexpr (SDDC_WV_LDSX >= 2) swap_halves_lds(R, R + 32, xl, lane);
 #pragma unroll
             for (int i = 0; i < 32; i++) {
-                if constexpr (SDDC_WV_LDSX < 2) swap32(R[i], R[32 + i]);
+                swap32(R[i], R[32 + i]);
                 s[i] = cadd(R[i], R[32 + i]);
                 d[i] = tw64<-1>(csub(R[i], R[32 + i]), i);
             }
@@ -361,10 +340,9 @@ __global__ __launch_bounds__(64, SDDC_WV_WAVES) void r2iq_wave_kernel(
         float2 Ye[32], Yo[32];
         {
             float2 s[32], d[32];
-            if constexpr (SDDC_WV_LDSX >= 2) swap_halves_lds(R, R + 32, xl, lane);
 #pragma unroll
             for (int i = 0; i < 32; i++) {
-                if constexpr (SDDC_WV_LDSX < 2) swap32(R[i], R[32 + i]);
+                swap32(R[i], R[32 + i]);
                 s[i] = cadd(R[i], R[32 + i]);
                 d[i] = tw64<+1>(csub(R[i], R[32 + i]), i);
             }
