@@ -224,7 +224,7 @@ def main() -> None:
         workload = f"single d={d} nblk={nblk}" + (f" fine_tune={args.fine_tune}" if args.fine_tune else "") \
             + (" cs16" if args.cs16 else "")
     else:
-        from extio_sddc_amd.shard import broadcast_samples, channel_shard
+        from extio_sddc_amd.shard import channel_shard
         tbs_all = [4 * c for c in range(args.channels)]
         lo, hi = channel_shard(args.channels, world, rank)
         tbs = tbs_all[lo:hi]
@@ -234,10 +234,18 @@ def main() -> None:
         per = output_samples(d, nblk) * 2
         d_out = torch.empty((nch_local, per), dtype=out_dtype, device=dev)
 
-        def step():
-            if world > 1:
-                broadcast_samples(d_in, src=0)
-            ddc.process_channels_device(d_in, nblk, tbs, d_out, stream)
+        if world > 1:
+            # the ingest rank's batch reaches every rank by RCCL broadcast over xGMI; batch
+            # i + 1's broadcast runs while batch i is processed (double-buffered input)
+            from extio_sddc_amd.shard import pipelined_batches
+            d_in2 = d_in.clone()
+            batches = pipelined_batches([d_in, d_in2], args.warmup + args.steps, src=0)
+
+            def step():
+                ddc.process_channels_device(next(batches), nblk, tbs, d_out, stream)
+        else:
+            def step():
+                ddc.process_channels_device(d_in, nblk, tbs, d_out, stream)
         samples_per_step_all = nblk * BLOCK          # one shared stream
         workload = f"channels d={d} nblk={nblk} nch={args.channels}" + (" cs16" if args.cs16 else "")
 

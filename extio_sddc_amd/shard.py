@@ -37,3 +37,35 @@ def broadcast_samples(buf, src: int = 0) -> None:
     import torch.distributed as dist
     assert buf.dtype == torch.int16 and buf.numel() % 2 == 0 and buf.is_contiguous()
     dist.broadcast(buf.view(torch.int32), src=src)
+
+
+def pipelined_batches(bufs, nbatches: int, src: int = 0, fill=None):
+    """Yield nbatches input batches, bufs[i % 2] for batch i, every rank receiving the src
+    rank's batch by broadcast, with the broadcast of batch i + 1 already in flight while the
+    caller processes batch i (overlap the xGMI broadcast with the compute).
+
+    bufs: two equal int16 buffers.  fill(buf, i): on the src rank, writes batch i into buf
+    before it is sent (None: the buffers already hold the batch, as in bench.py).
+    Ordering on a GPU: an async collective first waits for the work queued on the current
+    stream, so the broadcast into bufs[(i + 1) % 2] starts after batch i - 1 (the previous user
+    of that buffer) was processed; work.wait() makes the current stream wait for the data.
+    """
+    import torch
+    import torch.distributed as dist
+    assert len(bufs) == 2 and all(b.dtype == torch.int16 and b.numel() % 2 == 0 for b in bufs)
+    rank = dist.get_rank()
+
+    def send(i):
+        b = bufs[i % 2]
+        if fill is not None and rank == src:
+            fill(b, i)
+        return dist.broadcast(b.view(torch.int32), src=src, async_op=True)
+
+    if nbatches <= 0:
+        return
+    work = send(0)
+    for i in range(nbatches):
+        work.wait()
+        if i + 1 < nbatches:
+            work = send(i + 1)
+        yield bufs[i % 2]

@@ -6,6 +6,8 @@
 - channels (C5): rank 0 owns the int16 batch and broadcasts it (the xGMI/RCCL step on the
   GPU node; gloo here); each rank computes its contiguous channel shard; the gathered
   shards equal every channel computed on one rank.
+- pipelined broadcast (bench.py's C5 loop): with batch i + 1's broadcast in flight while batch
+  i is used, every rank still sees every batch, in order, with the src rank's content.
 The per-rank compute here is the oracle (no GPU); the partitioning, halo and collective
 logic is extio_sddc_amd.shard, the same code bench.py uses on the GPUs.
 """
@@ -53,6 +55,21 @@ def _worker(rank, world, port, mode, q):
                 full = O.r2iq(x, nblk, d, tb)
                 cat = np.concatenate([p[2] for p in sorted(parts, key=lambda p: p[0])])
                 q.put(bool(np.array_equal(cat, full)) and sum(p[1] - p[0] for p in parts) == nblk)
+        elif mode == "pipelined":
+            from extio_sddc_amd.shard import pipelined_batches
+            n = 5
+            bufs = [torch.zeros(4096 + 2 * 65536, dtype=torch.int16) for _ in range(2)]
+            stream = make_stream(2 * n, "uniform")
+
+            def fill(b, i):   # batch i = blocks [2i, 2i + 2) of one stream, with their halo
+                b.copy_(torch.from_numpy(stream[i * 2 * 65536:i * 2 * 65536 + b.numel()]))
+            seen = [b.numpy().copy() for b in pipelined_batches(bufs, n, src=0, fill=fill)]
+            ok = len(seen) == n and all(np.array_equal(seen[i], stream[i * 2 * 65536:i * 2 * 65536 + seen[i].size])
+                                        for i in range(n))
+            flags = [None] * world
+            dist.all_gather_object(flags, ok)
+            if rank == 0:
+                q.put(all(flags))
         else:
             nblk, d, nch = 2, 4, 6
             tbs = [4 * (97 * c % 1024) for c in range(nch)]
@@ -75,7 +92,7 @@ def _worker(rank, world, port, mode, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", ["segments", "channels"])
+@pytest.mark.parametrize("mode", ["segments", "channels", "pipelined"])
 def test_two_rank_gloo(mode):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
