@@ -1,0 +1,77 @@
+"""Seeded random parity sweep on a real MI355X (pytest -m gpu): 24 configurations drawn from
+d in 0..6, any legal tune bin (multiple of 4, the setFreqOffset grid, fft_mt_r2iq.cpp:104),
+sideband, rand, the synthetic sources and 1..5 blocks, each checked against the f64 oracle.
+At d = 0 the wave kernel (variant 3) is checked on the same case as well.
+
+Bar: IQ max-rel-err <= 1e-5 (north_star), or, where a float32 computation cannot reach it,
+<= 1.5 x the error of the oracle's float32 port (the reference's float arithmetic, restated) on
+the same case.  That happens when the channel holds nothing but the -120 dB stopband leakage
+of a strong out-of-band tone (the "bench" tone, tuned far away): max|r| is then tiny while the
+float32 rounding scales with the strong tone, and the f32 port itself is 1.4-1.7e-5 from
+float64 there (the GPU: 1.4-1.6e-5)."""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import pytest
+
+from extio_sddc_amd.synth import make_stream
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-5
+SOURCES = ["mix", "uniform", "bench", "oob"]
+
+
+def _cases(n=24, seed=0x5DDC):
+    rng = np.random.default_rng(seed)
+    out = []
+    for i in range(n):
+        d = int(rng.integers(0, 7)) if i >= 4 else 0           # a few d = 0 cases for the wave kernel
+        out.append((d, 4 * int(rng.integers(0, 1024)), int(rng.integers(0, 2)), int(rng.integers(0, 2)),
+                    SOURCES[int(rng.integers(0, len(SOURCES)))], int(rng.integers(1, 6)), int(rng.integers(1, 1 << 30))))
+    return out
+
+
+@pytest.fixture(scope="module")
+def ddc():
+    import torch
+    assert torch.cuda.is_available(), "gpu tests need a GPU"
+    from extio_sddc_amd import R2iq
+    r = R2iq(gain=1.0, device=0)
+    r._L.sddc_ddc_internal_set_variant.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    yield r
+    r.close()
+
+
+@pytest.fixture(scope="module")
+def H(oracle):
+    return oracle.filter_bank(1.0)
+
+
+@pytest.mark.parametrize("d,tb,lsb,rand,src,nblk,seed", _cases())
+def test_random_config_parity(ddc, oracle, H, d, tb, lsb, rand, src, nblk, seed):
+    import torch
+    from extio_sddc_amd import _lib, output_samples
+    x = make_stream(nblk, src, seed=seed)
+    r = oracle.r2iq(x, nblk, d, tb, lsb, rand, H=H)
+    y32 = oracle.r2iq(x, nblk, d, tb, lsb, rand, dtype=np.float32, H=oracle.filter_bank(1.0, np.float32))
+    bar = max(TOL, 1.5 * oracle.max_rel_err(y32, r))
+    d_in = torch.from_numpy(x).to("cuda")
+    for variant in ([0, 3] if d == 0 else [0]):
+        _lib.check(ddc._L.sddc_ddc_internal_set_variant(ddc._h, variant))
+        try:
+            ddc.setDecimate(d)
+            ddc.setTuneBin(tb)
+            ddc.setSideband(bool(lsb))
+            ddc.updateRand(bool(rand))
+            out = torch.full((output_samples(d, nblk) * 2,), float("nan"), dtype=torch.float32, device="cuda")
+            ddc.process_device(d_in, nblk, out)
+            torch.cuda.synchronize()
+        finally:
+            _lib.check(ddc._L.sddc_ddc_internal_set_variant(ddc._h, 0))
+        y = out.cpu().numpy().view(np.complex64)
+        assert np.all(np.isfinite(y))
+        err = oracle.max_rel_err(y, r)
+        assert err <= bar, f"variant {variant}: max-rel-err {err:.3e} (bar {bar:.3e})"
