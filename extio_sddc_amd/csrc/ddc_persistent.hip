@@ -494,6 +494,138 @@ __global__ __launch_bounds__(NT, SDDC_WAVES) void r2iq_persistent_kernel(
     }
 }
 
+// d = 0, two frames in flight per workgroup (internal variant 4).  Iteration f runs the forward
+// FFT of frame f and the inverse of frame f - 1 pass by pass, so one LDS exchange (write,
+// barrier, read) serves both: 3 exchanges and 6 barriers per frame instead of 5 and 10, and
+// every wave carries two independent dependency chains between barriers.  Forward passes
+// live in buffer P (Z stays there for the next iteration's split), inverse passes in Q:
+// 64 KB + 3.8 KB per workgroup, 2 workgroups (2 waves/SIMD) per CU.  The pipeline fill and
+// drain compute one garbage half each (uninitialised Z; stale input), never stored.
+#ifndef SDDC_PIPE_WAVES
+#define SDDC_PIPE_WAVES 2
+#endif
+template <bool RAND, bool NCO, bool CS16>
+__global__ __launch_bounds__(NT, SDDC_PIPE_WAVES) void r2iq_pipe_kernel(
+    const int *__restrict__ in32, void *__restrict__ out, int nframes, const float2 *__restrict__ tw_p1,
+    const float2 *__restrict__ tw_q1, const float2 *__restrict__ rec_f, const float4 *__restrict__ pq,
+    int tunebin, OutArgs oa, NcoArgs nco)
+{
+    constexpr int N = HALF;
+    __shared__ __attribute__((aligned(16))) float2 P[HALF];
+    __shared__ __attribute__((aligned(16))) float2 Q[HALF];
+    __shared__ __attribute__((aligned(16))) float2 twl[2 * 15 * 16];
+
+    const int tid = (int)threadIdx.x;
+    const int G = (int)gridDim.x, w = (int)blockIdx.x;
+    const int f0 = (int)(((long long)nframes * w) / G);
+    const int f1 = (int)(((long long)nframes * (w + 1)) / G);
+    if (f0 >= f1) return;
+
+    const float2 fw1_ = rec_f[tid], fw4_ = rec_f[NT + tid];
+    for (int i = tid; i < 2 * 15 * 16; i += NT) twl[i] = i < 15 * 16 ? tw_p1[i] : tw_q1[i - 15 * 16];
+
+    int blk = f0 / FRAMES, k = f0 - blk * FRAMES;   // forward frame
+    int gblk = blk, gk = k;                          // inverse frame (one behind)
+    int x[16];
+    load_frame(in32, blk, k, x);
+
+    for (int f = f0; f <= f1; f++) {
+        int z = 0;
+        asm volatile("" : "+s"(z));
+        const int t = tid + z;
+        const float4 *pqz = pq + z;
+        float2 fw1 = fw1_, fw4 = fw4_;
+        asm volatile("" : "+v"(fw1), "+v"(fw4));
+        const int sT = swz(t);
+        const int x15 = t & 15;
+        const int b1 = (t >> 4) * 256;
+        float2 v[16], u[16];
+        // ---- phase 0: forward pass 0 of f (input registers) | split x filter + inverse pass 0 of f-1 ----
+        {
+            float2 a[16];
+#pragma unroll
+            for (int r = 0; r < 16; r++)
+                a[r] = make_float2(derand<RAND>((int)(short)(x[r] & 0xffff)), derand<RAND>(x[r] >> 16));
+            if (++k == FRAMES) {
+                k = 0;
+                ++blk;
+            }
+            if (f + 1 < f1) load_frame(in32, blk, k, x);
+            DFT16<-1>(a, v);
+        }
+        {
+            const int b0 = tunebin + t;
+            const unsigned sb0b = 8u * (unsigned)swz(b0), sc0b = 8u * (unsigned)swz(HALF - b0);
+            const unsigned tb16 = 16u * (unsigned)t;
+            const char *pb = reinterpret_cast<const char *>(P);
+            const __amdgpu_buffer_rsrc_t rpq = buf_rsrc(pqz);
+            float2 a[16];
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int sh = NT * r - (NT * r >= N / 2 ? N : 0);
+                const float2 zk = *reinterpret_cast<const float2 *>(pb + ((sb0b + 8u * (unsigned)sh) & (8u * HALF - 8u)));
+                const float2 zc = *reinterpret_cast<const float2 *>(pb + ((sc0b - 8u * (unsigned)sh) & (8u * HALF - 8u)));
+                a[r] = split_pq(zk, zc, buf_load16(rpq, tb16, 16u * NT * r));
+            }
+            DFT16<+1>(a, u);
+        }
+        LOOP_SYNC();
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+            P[16 * t + (r ^ x15)] = v[r];
+            Q[16 * t + (r ^ x15)] = u[r];
+        }
+        LOOP_SYNC();
+        // ---- phase 1: pass 1 of both (table twiddles W_256^{(t%16) r}) ----
+        {
+            float2 a[16], c[16];
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                a[r] = P[sT + NT * r];
+                c[r] = Q[sT + NT * r];
+            }
+#pragma unroll
+            for (int r = 1; r < 16; r++) {
+                a[r] = TW<-1>(a[r], twl[(r - 1) * 16 + x15]);
+                c[r] = TW<+1>(c[r], twl[15 * 16 + (r - 1) * 16 + x15]);
+            }
+            DFT16<-1>(a, v);
+            DFT16<+1>(c, u);
+        }
+        LOOP_SYNC();
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+            P[b1 + 16 * r + (x15 ^ r)] = v[r];
+            Q[b1 + 16 * r + (x15 ^ r)] = u[r];
+        }
+        LOOP_SYNC();
+        // ---- phase 2: forward pass 2 of f -> Z | inverse pass 2 of f-1 -> overlap-discard store ----
+        {
+            float2 a[16], c[16];
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                a[r] = P[sT + NT * r];
+                c[r] = Q[sT + NT * r];
+            }
+            TWREC16<-1>(a, fw1, fw4);
+            TWREC16<+1>(c, fw1, fw4);
+            DFT16<-1>(a, v);
+            DFT16<+1>(c, u);
+        }
+        if (f > f0) {
+            emit_frame<N / 16, NCO, CS16>(out, gblk * 8 * N + emit_base<N>(gk), gk, t, u, oa, nco);
+            if (++gk == FRAMES) {
+                gk = 0;
+                ++gblk;
+            }
+        }
+        LOOP_SYNC();
+#pragma unroll
+        for (int r = 0; r < 16; r++) P[sT + NT * r] = v[r];   // Z, natural order
+        LOOP_SYNC();
+    }
+}
+
 // Split x filter coefficients for one (d, tunebin): pq[m] = (P, Q) of inverse input m, with
 // bin = tb + m - (m >= N/2 ? N : 0) (fft_mt_r2iq_impl.hpp:84-98); zero outside [0, 4096).
 // Evaluated in double from the float tables and rounded once.
@@ -570,7 +702,47 @@ hipError_t launch_d(const KernelTables &t, const Launch &L, int rand, bool cs16)
     return nco ? launch_f<D, false, true>(t, L, cs16) : launch_f<D, false, false>(t, L, cs16);
 }
 
+int g_pipe_occ[8] = {};
+
+template <bool RAND, bool NCO, bool CS16>
+hipError_t launch_pipe(const KernelTables &t, const Launch &L)
+{
+    auto kern = r2iq_pipe_kernel<RAND, NCO, CS16>;
+    int &occ = g_pipe_occ[(RAND ? 4 : 0) + (NCO ? 2 : 0) + (CS16 ? 1 : 0)];
+    if (occ == 0) {
+        int nb = 0;
+        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, NT, 0);
+        if (e != hipSuccess) return e;
+        e = hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, L.device);
+        if (e != hipSuccess) return e;
+        occ = nb > 0 ? nb : 1;
+    }
+    const int nframes = L.nblk * FRAMES;
+    int grid = g_cus * occ;
+    if (grid > nframes) grid = nframes;
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), 0, L.s, reinterpret_cast<const int *>(L.d_in), L.d_out,
+                       nframes, t.tw_p1, t.tw_q1[0], t.rec_f, L.pq, L.tunebin, L.oa, L.nco);
+    return hipGetLastError();
+}
+
+template <bool RAND, bool NCO>
+hipError_t launch_pipe_f(const KernelTables &t, const Launch &L, bool cs16)
+{
+    return cs16 ? launch_pipe<RAND, NCO, true>(t, L) : launch_pipe<RAND, NCO, false>(t, L);
+}
+
 }  // namespace
+
+hipError_t launch_frames_pipelined(const KernelTables &t, const int16_t *d_in, int nblk, void *d_out,
+                                   const float4 *pq, int tunebin, int lsb, int rand, int cs16, float cs16_scale,
+                                   const float2 *nco_starts, const float2 *nco_trig, int device, hipStream_t s)
+{
+    const Launch L{d_in, nblk, d_out, pq, tunebin, device, s, OutArgs{lsb ? 0x80000000u : 0u, cs16_scale},
+                   NcoArgs{nco_starts, nco_trig}};
+    const bool f = cs16 != 0, nco = nco_starts != nullptr;
+    if (rand) return nco ? launch_pipe_f<true, true>(t, L, f) : launch_pipe_f<true, false>(t, L, f);
+    return nco ? launch_pipe_f<false, true>(t, L, f) : launch_pipe_f<false, false>(t, L, f);
+}
 
 hipError_t launch_build_split_filter(const KernelTables &t, int d, int tunebin, float4 *pq, hipStream_t s)
 {

@@ -1,7 +1,8 @@
 """Seeded random parity sweep on a real MI355X (pytest -m gpu): 24 configurations drawn from
 d in 0..6, any legal tune bin (multiple of 4, the setFreqOffset grid, fft_mt_r2iq.cpp:104),
 sideband, rand, the synthetic sources and 1..5 blocks, each checked against the f64 oracle.
-At d = 0 the wave kernel (variant 3) is checked on the same case as well.
+At d = 0 the wave kernel (variant 3) and the two-frame pipelined kernel (variant 4) are checked
+on the same case as well.
 
 Bar: IQ max-rel-err <= 1e-5 (north_star), or, where a float32 computation cannot reach it,
 <= 1.5 x the error of the oracle's float32 port (the reference's float arithmetic, restated) on
@@ -59,7 +60,7 @@ def test_random_config_parity(ddc, oracle, H, d, tb, lsb, rand, src, nblk, seed)
     y32 = oracle.r2iq(x, nblk, d, tb, lsb, rand, dtype=np.float32, H=oracle.filter_bank(1.0, np.float32))
     bar = max(TOL, 1.5 * oracle.max_rel_err(y32, r))
     d_in = torch.from_numpy(x).to("cuda")
-    for variant in ([0, 3] if d == 0 else [0]):
+    for variant in ([0, 3, 4] if d == 0 else [0]):
         _lib.check(ddc._L.sddc_ddc_internal_set_variant(ddc._h, variant))
         try:
             ddc.setDecimate(d)

@@ -1,9 +1,12 @@
-"""The d = 0 wave kernel (ddc_wave.hip, internal variant 3) against the oracle and against the
-default persistent-workgroup kernel (variant 0), on a real MI355X (pytest -m gpu).
+"""The alternative d = 0 kernels against the oracle and against the default persistent-workgroup
+kernel (variant 0), on a real MI355X (pytest -m gpu): the wave kernel (ddc_wave.hip, internal
+variant 3) and the two-frames-in-flight persistent kernel (ddc_persistent.hip
+r2iq_pipe_kernel, variant 4).
 
-Cases specific to its layout: every tune-bin class of its per-lane tables (bins whose mirror
-is in lane 0 / lane 32, zero-filled bins below 0 and above 4095), sideband / rand / CS16 /
-fused NCO output stages, the frame-to-wave split of the persistent grid, and kernel-vs-kernel
+Cases specific to their layouts: every tune-bin class of the wave kernel's per-lane tables
+(bins whose mirror is in lane 0 / lane 32, zero-filled bins below 0 and above 4095), sideband /
+rand / CS16 / fused NCO output stages, the frame split of the persistent grid (including
+workgroups of one frame, where the pipeline is all fill and drain), and kernel-vs-kernel
 agreement at the BASELINE size.  Bar: IQ max-rel-err <= 1e-5 (north_star).
 """
 from __future__ import annotations
@@ -18,6 +21,7 @@ from extio_sddc_amd.synth import make_stream
 pytestmark = pytest.mark.gpu
 
 TOL = 1e-5
+VARIANTS = [3, 4]
 
 
 @pytest.fixture(scope="module")
@@ -69,45 +73,49 @@ def run(torch, ddc, d_in, nblk, tb, lsb=0, rand=0, variant=3):
 TBS = [0, 4, 60, 64, 96, 284, 1024, 1228, 2016, 2048, 2080, 3684, 3888, 4032, 4092]
 
 
+@pytest.mark.parametrize("variant", VARIANTS)
 @pytest.mark.parametrize("tb", TBS)
-def test_wave_parity_tunebins(torch_dev, ddc, oracle, H, tb):
+def test_wave_parity_tunebins(torch_dev, ddc, oracle, H, tb, variant):
     nblk = 3
     x = make_stream(nblk, "mix")
-    y = run(torch_dev, ddc, torch_dev.from_numpy(x).to("cuda"), nblk, tb).cpu().numpy().view(np.complex64)
+    y = run(torch_dev, ddc, torch_dev.from_numpy(x).to("cuda"), nblk, tb, variant=variant).cpu().numpy().view(np.complex64)
     r = oracle.r2iq(x, nblk, 0, tb, H=H)
     assert np.all(np.isfinite(y))
     err = oracle.max_rel_err(y, r)
     assert err <= TOL, f"tb {tb}: max-rel-err {err:.3e}"
 
 
+@pytest.mark.parametrize("variant", VARIANTS)
 @pytest.mark.parametrize("src,lsb,rand", [("uniform", 0, 1), ("uniform", 1, 1), ("oob", 1, 0), ("bench", 0, 0)])
-def test_wave_parity_sources(torch_dev, ddc, oracle, H, src, lsb, rand):
+def test_wave_parity_sources(torch_dev, ddc, oracle, H, src, lsb, rand, variant):
     nblk = 4
     x = make_stream(nblk, src)
-    y = run(torch_dev, ddc, torch_dev.from_numpy(x).to("cuda"), nblk, 1024, lsb, rand).cpu().numpy().view(np.complex64)
+    y = run(torch_dev, ddc, torch_dev.from_numpy(x).to("cuda"), nblk, 1024, lsb, rand, variant).cpu().numpy().view(np.complex64)
     r = oracle.r2iq(x, nblk, 0, 1024, lsb, rand, H=H)
     err = oracle.max_rel_err(y, r)
     assert err <= TOL, f"{src} lsb={lsb} rand={rand}: max-rel-err {err:.3e}"
 
 
-@pytest.mark.parametrize("nblk", [1, 2, 5, 37])
-def test_wave_frame_split(torch_dev, ddc, oracle, H, nblk):
+@pytest.mark.parametrize("variant", VARIANTS)
+@pytest.mark.parametrize("nblk", [1, 2, 5, 37, 100])
+def test_wave_frame_split(torch_dev, ddc, oracle, H, nblk, variant):
     """Grids smaller than, equal to and larger than the frame count: every frame lands once."""
     x = make_stream(nblk, "mix", seed=nblk)
-    y = run(torch_dev, ddc, torch_dev.from_numpy(x).to("cuda"), nblk, 2048).cpu().numpy().view(np.complex64)
+    y = run(torch_dev, ddc, torch_dev.from_numpy(x).to("cuda"), nblk, 2048, variant=variant).cpu().numpy().view(np.complex64)
     r = oracle.r2iq(x, nblk, 0, 2048, H=H)
     assert oracle.max_rel_err(y, r) <= TOL
 
 
-def test_wave_vs_persistent_full_size(torch_dev, ddc):
-    """BASELINE size (2048 blocks): the wave kernel and the persistent kernel agree to 1e-5, and
-    the wave kernel over 8 halo'd segments equals one launch bit for bit."""
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_wave_vs_persistent_full_size(torch_dev, ddc, variant):
+    """BASELINE size (2048 blocks): the alternative kernel and the persistent kernel agree to 1e-5,
+    and the alternative kernel over 8 halo'd segments equals one launch bit for bit."""
     torch = torch_dev
     nblk, seg = 2048, 256
     g = torch.Generator(device="cuda").manual_seed(0x5DDC)
     d_in = torch.randint(-32768, 32767, (4096 + nblk * 65536,), dtype=torch.int16, device="cuda", generator=g)
     d_in[:4096] = 0
-    yw = run(torch, ddc, d_in, nblk, 1024, variant=3)
+    yw = run(torch, ddc, d_in, nblk, 1024, variant=variant)
     yp = run(torch, ddc, d_in, nblk, 1024, variant=0)
     assert torch.isfinite(yw).all()
     err = ((yw - yp).abs().max() / yp.abs().max()).item()
@@ -116,7 +124,7 @@ def test_wave_vs_persistent_full_size(torch_dev, ddc):
     per = output_samples(0, seg) * 2
     parts = torch.empty_like(yw)
     for s in range(nblk // seg):
-        parts[s * per:(s + 1) * per] = run(torch, ddc, d_in[s * seg * 65536:], seg, 1024)
+        parts[s * per:(s + 1) * per] = run(torch, ddc, d_in[s * seg * 65536:], seg, 1024, variant=variant)
     assert torch.equal(yw, parts)
 
 
@@ -144,18 +152,19 @@ def _run_fmt(torch, ddc, d_in, nblk, tb, variant, cs16_scale=None, fc=0.0):
     return out
 
 
-def test_wave_output_stages(torch_dev, ddc):
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_wave_output_stages(torch_dev, ddc, variant):
     """CS16 and the fused fine-tune NCO through the wave kernel: CS16 = saturate(rint(x * scale))
     of its own CF32 output (bit-exact); NCO-on output within 1e-5 of the persistent kernel's."""
     torch = torch_dev
     nblk, tb = 6, 1228
     x = torch.from_numpy(make_stream(nblk, "mix")).to("cuda")
-    cf = _run_fmt(torch, ddc, x, nblk, tb, 3)
+    cf = _run_fmt(torch, ddc, x, nblk, tb, variant)
     scale = 3e4 / cf.abs().max().item()
-    cs = _run_fmt(torch, ddc, x, nblk, tb, 3, cs16_scale=scale)
+    cs = _run_fmt(torch, ddc, x, nblk, tb, variant, cs16_scale=scale)
     ref = torch.clamp(torch.round(cf * torch.tensor(scale, dtype=torch.float32)), -32768, 32767).to(torch.int16)
     assert torch.equal(cs, ref)
-    yw = _run_fmt(torch, ddc, x, nblk, tb, 3, fc=0.0123)
+    yw = _run_fmt(torch, ddc, x, nblk, tb, variant, fc=0.0123)
     yp = _run_fmt(torch, ddc, x, nblk, tb, 0, fc=0.0123)
     assert torch.isfinite(yw).all()
     err = ((yw - yp).abs().max() / yp.abs().max()).item()
