@@ -43,6 +43,10 @@ hipError_t launch_build_split_filter(const KernelTables &t, int d, int tunebin, 
 hipError_t launch_frames_pipelined(const KernelTables &t, const int16_t *d_in, int nblk, void *d_out,
                                    const float4 *pq, int tunebin, int lsb, int rand, int cs16, float cs16_scale,
                                    const float2 *nco_starts, const float2 *nco_trig, int device, hipStream_t s);
+// d = 0 only: radix 8, 512 threads per frame (8 points per thread); same arguments and tables.
+hipError_t launch_frames_r8(const KernelTables &t, const int16_t *d_in, int nblk, void *d_out, const float4 *pq,
+                            int tunebin, int lsb, int rand, int cs16, float cs16_scale, const float2 *nco_starts,
+                            const float2 *nco_trig, int device, hipStream_t s);
 
 // d = 0 wave kernel (ddc_wave.hip): one wave64 per frame, 64 points per lane.  pqW (4096
 // float4) and twI (4096 float2) are its per-tunebin tables, built by launch_build_wave_tables.

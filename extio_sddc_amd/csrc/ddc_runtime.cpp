@@ -77,7 +77,8 @@ struct sddc_ddc {
     int d = 0, lsb = 0, rand = 0, tunebin = SDDC_DDC_HALF_FFT / 4;   // ctor: mtunebin = halfFft/4
     int variant = 0;                       // 0: persistent (v2); 1: one workgroup per frame (v1);
                                            // 3: one wave per frame at d = 0 (ddc_wave.hip), 4: two frames in
-                                           // flight per workgroup at d = 0; persistent otherwise
+                                           // flight per workgroup at d = 0, 5: radix 8 x 512 threads at
+                                           // d = 0; persistent otherwise
     int out_fmt = SDDC_DDC_FMT_CF32;       // output stage format
     float cs16_scale = 1.f;
     sddc::KernelTables tables;
@@ -450,7 +451,10 @@ static hipError_t launch_single(sddc_ddc_t *h, const int16_t *d_in, int nblk, vo
         h->pq_tb = h->tunebin;
     }
     const float2 *nco_starts = nco ? h->d_nco + sddc::FineTune::kTable : nullptr, *nco_trig = nco ? h->d_nco : nullptr;
-    hipError_t e = h->d == 0 && h->variant == 4
+    hipError_t e = h->d == 0 && h->variant == 5
+        ? sddc::launch_frames_r8(h->tables, d_in, nblk, d_out, h->d_pq, h->tunebin, h->lsb, h->rand,
+                                 h->out_fmt == SDDC_DDC_FMT_CS16, h->cs16_scale, nco_starts, nco_trig, h->device, s)
+        : h->d == 0 && h->variant == 4
         ? sddc::launch_frames_pipelined(h->tables, d_in, nblk, d_out, h->d_pq, h->tunebin, h->lsb, h->rand,
                                         h->out_fmt == SDDC_DDC_FMT_CS16, h->cs16_scale, nco_starts, nco_trig,
                                         h->device, s)
@@ -490,7 +494,7 @@ int sddc_ddc_set_fine_tune(sddc_ddc_t *h, float relative_freq)
 /* internal (not in include/sddc_ddc.h): kernel variant for A/B timing, see sddc_ddc_internal.h */
 int sddc_ddc_internal_set_variant(sddc_ddc_t *h, int variant)
 {
-    if (!h || variant < 0 || variant > 4 || variant == 2) return fail(SDDC_ERR_ARG, "bad variant");
+    if (!h || variant < 0 || variant > 5 || variant == 2) return fail(SDDC_ERR_ARG, "bad variant");
     h->variant = variant;
     return SDDC_OK;
 }

@@ -60,7 +60,7 @@ def test_random_config_parity(ddc, oracle, H, d, tb, lsb, rand, src, nblk, seed)
     y32 = oracle.r2iq(x, nblk, d, tb, lsb, rand, dtype=np.float32, H=oracle.filter_bank(1.0, np.float32))
     bar = max(TOL, 1.5 * oracle.max_rel_err(y32, r))
     d_in = torch.from_numpy(x).to("cuda")
-    for variant in ([0, 3, 4] if d == 0 else [0]):
+    for variant in ([0, 3, 4, 5] if d == 0 else [0]):
         _lib.check(ddc._L.sddc_ddc_internal_set_variant(ddc._h, variant))
         try:
             ddc.setDecimate(d)
