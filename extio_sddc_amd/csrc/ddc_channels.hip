@@ -5,7 +5,9 @@
 // frame's forward transform ONCE (as ddc_persistent.hip: 3 x radix-16 Stockham in 32 KB
 // of swizzled LDS, int16 -> float with optional RAND), then walks the chunk G = 256/TPC
 // channels at a time, TPC = N/16 threads per channel:
-//   pass A  r2c split x filter for the channel's N bins around its tune bin
+//   split   the r2c split X2[bin] = (Z_k + conj Z_-k) - i W_8192^bin (Z_k - conj Z_-k) once per
+//           item, for the bins the chunk's channels read (fft_mt_r2iq_impl.hpp:88 gives X)
+//   pass A  filter multiply X2[tb + m] * H[m]/2 for the channel's N bins around its tune bin
 //           (Core/fft_mt_r2iq_impl.hpp:76-96), DFT-16 in registers, -> per-channel LDS slice
 //   pass B  radix-(N/16) Stockham step with W_256 twiddles from LDS, overlap-discard
 //           write of the kept outputs to the channel's stream (impl.hpp:117-138)
@@ -15,7 +17,6 @@
 
 #include <algorithm>
 
-#include "ddc_consts.h"
 #include "ddc_kernels.h"
 #include "fft_device.hpp"
 #include "ddc_device_io.hpp"
@@ -29,7 +30,7 @@ constexpr int HOP = 6144;
 constexpr int BLOCK = 65536;
 constexpr int FRAMES = 11;
 constexpr int CHUNK = 128;    // channels per work item
-constexpr int ZC_MAX = 1536;  // compact window of forward bins per chunk (window + its mirror)
+constexpr int ZC_MAX = 1536;  // compact window of split bins per chunk
 
 __device__ __forceinline__ int swz(int e) { return e ^ ((e >> 4) & 15); }
 
@@ -88,17 +89,20 @@ __device__ __forceinline__ void twiddle_rec16(float2 *a, float2 w1, float2 w4)
     a[15] = cmul(a[15], cmul(w12, w3));
 }
 
-template <int N>
-__device__ __forceinline__ constexpr float2 wsplit(int r)
+// 2 X[k] = (Z_k + conj Z_-k) - i W_8192^k (Z_k - conj Z_-k), Z = FFT4096(x_even + i x_odd)
+__device__ __forceinline__ float2 split2(float2 zk, float2 zc, float2 wk)
 {
-    if constexpr (N == 256) return make_float2(kWsplitRe256[r], kWsplitIm256[r]);
-    else if constexpr (N == 128) return make_float2(kWsplitRe128[r], kWsplitIm128[r]);
-    else return make_float2(kWsplitRe64[r], kWsplitIm64[r]);
+    const float2 A = make_float2(zk.x + zc.x, zk.y - zc.y);
+    const float2 Bi = make_float2(zk.y + zc.y, zc.x - zk.x);   // (Zk - conj Zc)/i
+    return cadd(A, cmul(Bi, wk));
 }
 
-// COMPACT: after the forward transform the chunk's bins [lo, lo + w) and their mirrors are
-// copied into a window zcw (host-checked to fit ZC_MAX), and the per-channel slices reuse the
-// transform buffer: 48 KB of LDS instead of 68 KB, three workgroups per CU instead of two.
+// The r2c split is evaluated once per item and shared by the chunk's channels: a channel bin
+// then costs one LDS read and one complex multiply (it was two reads and ~20 VALU per channel).
+// COMPACT: the split spectrum of the chunk's bins [lo, lo + w) (host-checked to fit ZC_MAX)
+// goes into a window xw with N/2 zeros either side, so every channel bin, in band or not, reads
+// xw[bin - lo + N/2] without a range test; the per-channel slices reuse the transform buffer
+// (3 workgroups per CU).  Otherwise the split is done in place over all 4096 bins.
 template <int D, bool RAND, bool CS16, bool COMPACT>
 __global__ __launch_bounds__(NT, 2) void r2iq_channels_v2_kernel(
     const int *__restrict__ in32, void *__restrict__ out, size_t stride, int nframes,
@@ -114,12 +118,11 @@ __global__ __launch_bounds__(NT, 2) void r2iq_channels_v2_kernel(
     constexpr int BPT = 16 / TPC;        // pass-B butterflies per thread
 
     static_assert(G * N == HALF, "per-channel slices fill exactly one transform buffer");
-    __shared__ __attribute__((aligned(16))) float2 zbuf[COMPACT ? HALF + ZC_MAX : 2 * HALF];
-    float2 *const zl = zbuf;                              // forward transform
+    __shared__ __attribute__((aligned(16))) float2 zbuf[COMPACT ? HALF + ZC_MAX + N : 2 * HALF];
+    float2 *const zl = zbuf;                              // forward transform, then (!COMPACT) X2
     float2 *const work = COMPACT ? zbuf : zbuf + HALF;    // channel slices (reuse zl when COMPACT)
-    float2 *const zcw = zbuf + HALF;                      // COMPACT: [window | mirror window]
+    float2 *const xw = zbuf + HALF;                       // COMPACT: [N/2 zeros | X2 window | N/2 zeros]
     __shared__ __attribute__((aligned(16))) float2 twl[15 * 16];
-    __shared__ __attribute__((aligned(16))) float2 hl[N];
 
     const int tid = (int)threadIdx.x;
     const int nchunks = (nch + CHUNK - 1) / CHUNK;
@@ -127,9 +130,11 @@ __global__ __launch_bounds__(NT, 2) void r2iq_channels_v2_kernel(
     const int i0 = (int)(items * blockIdx.x / gridDim.x), i1 = (int)(items * (blockIdx.x + 1) / gridDim.x);
     if (i0 >= i1) return;
     for (int i = tid; i < 15 * 16; i += NT) twl[i] = tw_p1[i];
-    for (int i = tid; i < N; i += NT) hl[i] = hsel[i];
     const float2 fw1_ = rec_f[tid], fw4_ = rec_f[NT + tid];
     const int l_ = tid % TPC, g_ = tid / TPC;
+    float2 hr[16];   // this thread's filter taps H[m]/2, m = l + TPC r, for every channel and frame
+#pragma unroll
+    for (int r = 0; r < 16; r++) hr[r] = hsel[l_ + TPC * r];
 
     for (int it = i0; it < i1; it++) {
         int z = 0;
@@ -152,7 +157,7 @@ __global__ __launch_bounds__(NT, 2) void r2iq_channels_v2_kernel(
             }
             dft16<-1>(a, v);
         }
-        __syncthreads();   // previous item's readers of zl / twl / hl done
+        __syncthreads();   // previous item's readers of zl / twl done
 #pragma unroll
         for (int r = 0; r < 16; r++) zl[16 * t + (r ^ x15)] = v[r];
         __syncthreads();
@@ -182,19 +187,28 @@ __global__ __launch_bounds__(NT, 2) void r2iq_channels_v2_kernel(
 #pragma unroll
         for (int r = 0; r < 16; r++) zl[sT + NT * r] = v[r];
         __syncthreads();
-        int lo = 0, lo2 = 0, w1 = 0;
+        int lo = 0;
         if constexpr (COMPACT) {
-            // bins [lo, lo + w1) of this chunk's channels, then their mirrors (4096 - b) & 4095,
-            // which run contiguously (mod 4096) from lo2 = (4097 - lo - w1) & 4095
+            // X2 of bins [lo, lo + w1) of this chunk's channels at xw[N/2 + bin - lo]
             const int2 wv = windows[chunk];
             lo = wv.x;
-            w1 = wv.y;
-            lo2 = (HALF + 1 - lo - w1) & (HALF - 1);
-            for (int i = t; i < 2 * w1; i += NT) {
-                const int bin = i < w1 ? lo + i : (lo2 + i - w1) & (HALF - 1);
-                zcw[i] = zl[swz(bin)];
+            const int w1 = wv.y;
+            for (int i = t; i < w1 + N; i += NT) {
+                const int bin = lo + i - N / 2;
+                float2 x2 = make_float2(0.f, 0.f);
+                if (i >= N / 2 && i < N / 2 + w1) x2 = split2(zl[swz(bin)], zl[swz((HALF - bin) & (HALF - 1))], post8192[bin]);
+                xw[i] = x2;
             }
             __syncthreads();   // zl is overwritten by the channel slices from here on
+        } else {
+            // in place over all bins: thread-owned pairs (k, 4096 - k)
+            for (int k0 = t; k0 <= HALF / 2; k0 += NT) {
+                const int k1 = (HALF - k0) & (HALF - 1);
+                const float2 z0 = zl[swz(k0)], z1 = zl[swz(k1)];
+                zl[swz(k0)] = split2(z0, z1, post8192[k0]);
+                if (k1 != k0) zl[swz(k1)] = split2(z1, z0, post8192[k1]);
+            }
+            __syncthreads();
         }
 
         // ---------------- channels, G at a time ----------------
@@ -204,33 +218,23 @@ __global__ __launch_bounds__(NT, 2) void r2iq_channels_v2_kernel(
         for (int cg = cbeg; cg < cend; cg += G) {
             const int c = cg + g;
             const bool cok = c < cend;
-            const int tb = cok ? tunebins[c] : 0;
-            // pass A: bins tb + m (- N), m = l + TPC r; split x filter; DFT-16
+            const int tb = cok ? tunebins[c] : lo;   // idle lanes read in-range, never store
+            // pass A: bins tb + m (- N), m = l + TPC r; X2 x filter; DFT-16
             {
-                const float2 pbc = post8192[(tb + l) & 8191];     // W_8192^{tb + l}
                 float2 a[16];
+                const float2 *xb = xw + (tb - lo + N / 2 + l);   // COMPACT: xb[TPC r - N wrap]
 #pragma unroll
                 for (int r = 0; r < 16; r++) {
                     const int m = l + TPC * r;
                     const bool wrap = TPC * r >= N / 2;
-                    const int bin = tb + m - (wrap ? N : 0);
-                    const bool ok = cok && (unsigned)bin < (unsigned)HALF;
-                    float2 zk, zc;
                     if constexpr (COMPACT) {
-                        // out-of-window bins only occur for !ok legs (masked below); clamp the index
-                        const int i1 = min(max(bin - lo, 0), w1 - 1);
-                        const int i2 = min(max(((HALF - bin) - lo2) & (HALF - 1), 0), w1 - 1);
-                        zk = zcw[i1];
-                        zc = zcw[w1 + i2];
+                        a[r] = cmul(xb[TPC * r - (wrap ? N : 0)], hr[r]);   // zero out of band
                     } else {
-                        zk = zl[swz(bin & (HALF - 1))];
-                        zc = zl[swz((HALF - bin) & (HALF - 1))];
+                        const int bin = tb + m - (wrap ? N : 0);
+                        const bool ok = (unsigned)bin < (unsigned)HALF;
+                        const float2 val = cmul(zl[swz(bin & (HALF - 1))], hr[r]);
+                        a[r] = ok ? val : make_float2(0.f, 0.f);
                     }
-                    const float2 A = make_float2(zk.x + zc.x, zk.y - zc.y);
-                    const float2 Bi = make_float2(zk.y + zc.y, zc.x - zk.x);   // (Zk - conj Zc)/i
-                    const float2 wb = cmul(pbc, wsplit<N>(r));
-                    const float2 val = cmul(cadd(A, cmul(Bi, wb)), hl[m]);
-                    a[r] = ok ? val : make_float2(0.f, 0.f);
                 }
                 float2 u[16];
                 dft16<+1>(a, u);
@@ -345,7 +349,7 @@ bool channel_windows(int d, const int *tunebins, int nch, int2 *windows)
             mx = std::max(mx, tunebins[c]);
         }
         const int lo = std::max(0, mn - N / 2), hi = std::min(HALF, mx + N / 2);
-        if (2 * (hi - lo) > ZC_MAX) return false;
+        if (hi - lo > ZC_MAX) return false;
         windows[k] = make_int2(lo, hi - lo);
     }
     return true;
