@@ -1,7 +1,8 @@
 // ddc_channels.hip — many-channel DDC for gfx950 (up to 1024
-// tune offsets of one stream, d >= 4 i.e. mfft N <= 256).
+// tune offsets of one stream).  r2iq_channels_v2_kernel covers d >= 4 (mfft N <= 256),
+// r2iq_channels_p_kernel (below) d = 0..3.
 //
-// Work item = (frame, chunk of <= 128 channels).  Per item the workgroup computes the
+// v2: work item = (frame, chunk of <= 128 channels).  Per item the workgroup computes the
 // frame's forward transform ONCE (as ddc_persistent.hip: 3 x radix-16 Stockham in 32 KB
 // of swizzled LDS, int16 -> float with optional RAND), then walks the chunk G = 256/TPC
 // channels at a time, TPC = N/16 threads per channel:
@@ -286,7 +287,180 @@ __global__ __launch_bounds__(NT, 2) void r2iq_channels_v2_kernel(
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// Many channels at d = 0..3 (N = 4096 >> d >= 512): persistent, work item = (frame, chunk of
+// <= CHUNK_P channels).  Per item the forward transform (as ddc_persistent.hip) and the
+// shared r2c split X2 in place over all bins (buffer zl), then the channels CG = 2^d at a
+// time, so every inverse pass keeps all 256 threads busy with 16 points each:
+//   pass 0  radix N/256 per channel (each thread: CG channels x N/256 bins; the filter taps of
+//           its bins live in registers), into the channels' N-element slices of `wi`
+//   pass 1  radix 16, NS = N/256: thread t -> channel t / (N/16), butterfly t % (N/16)
+//   pass 2  radix 16, NS = N/16, register-recurrence twiddles, overlap-discard store
+// 32 KB transform + 32 KB of channel slices + twiddles: 2 workgroups per CU.
+constexpr int CHUNK_P = 32;
+
+template <int D, bool RAND, bool CS16>
+__global__ __launch_bounds__(NT, 2) void r2iq_channels_p_kernel(
+    const int *__restrict__ in32, void *__restrict__ out, size_t stride, int nframes,
+    const int *__restrict__ tunebins, int nch, const float2 *__restrict__ tw_p1, const float2 *__restrict__ tw_q1,
+    const float2 *__restrict__ rec_f, const float2 *__restrict__ rec_i, const float2 *__restrict__ post8192,
+    const float2 *__restrict__ hsel, OutArgs oa)
+{
+    constexpr int N = HALF >> D;
+    static_assert(N >= 512, "d = 0..3");
+    constexpr int R0 = N / 256;          // inverse pass-0 radix
+    constexpr int NB = N / 16;           // radix-16 butterflies per channel in passes 1, 2
+    constexpr int CG = NT / NB;          // channels in flight (2^d)
+    __shared__ __attribute__((aligned(16))) float2 zl[HALF];
+    __shared__ __attribute__((aligned(16))) float2 wi[CG * N];
+    __shared__ __attribute__((aligned(16))) float2 twl[15 * 16 + 15 * R0];
+
+    const int tid = (int)threadIdx.x;
+    const int nchunks = (nch + CHUNK_P - 1) / CHUNK_P;
+    const long long items = (long long)nframes * nchunks;
+    const int i0 = (int)(items * blockIdx.x / gridDim.x), i1 = (int)(items * (blockIdx.x + 1) / gridDim.x);
+    if (i0 >= i1) return;
+    for (int i = tid; i < 15 * 16 + 15 * R0; i += NT) twl[i] = i < 15 * 16 ? tw_p1[i] : tw_q1[i - 15 * 16];
+    const float2 fw1_ = rec_f[tid], fw4_ = rec_f[NT + tid];
+    const int jb_ = tid % NB, cb_ = tid / NB;    // passes 1, 2: butterfly, channel in group
+    const float2 iw1_ = rec_i[jb_], iw4_ = rec_i[NT + jb_];
+    float2 hr[R0];   // H[m]/2 for this thread's pass-0 bins m = t + 256 r
+#pragma unroll
+    for (int r = 0; r < R0; r++) hr[r] = hsel[tid + NT * r];
+
+    for (int it = i0; it < i1; it++) {
+        int z = 0;
+        asm volatile("" : "+s"(z));
+        const int t = tid + z, jb = jb_ + z, cb = cb_ + z;
+        float2 fw1 = fw1_, fw4 = fw4_, iw1 = iw1_, iw4 = iw4_;
+        asm volatile("" : "+v"(fw1), "+v"(fw4), "+v"(iw1), "+v"(iw4));
+        const int f = it / nchunks, chunk = it - f * nchunks;
+        const int blk = f / FRAMES, k = f - blk * FRAMES;
+        const int sT = swz(t), x15 = t & 15;
+        // ---------------- forward: Z = FFT4096(x_even + i x_odd) in zl ----------------
+        float2 v[16];
+        {
+            const __amdgpu_buffer_rsrc_t rs = buf_rsrc(in32 + ((size_t)blk * BLOCK + (size_t)k * HOP) / 2);
+            float2 a[16];
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const int w = buf_load4<SDDC_LD_AUX>(rs, 4u * (unsigned)t, 4u * NT * r);
+                a[r] = make_float2(derand<RAND>((int)(short)(w & 0xffff)), derand<RAND>(w >> 16));
+            }
+            dft16<-1>(a, v);
+        }
+        __syncthreads();   // the previous item's readers of zl / wi are done
+#pragma unroll
+        for (int r = 0; r < 16; r++) zl[16 * t + (r ^ x15)] = v[r];
+        __syncthreads();
+        {
+            float2 a[16];
+#pragma unroll
+            for (int r = 0; r < 16; r++) a[r] = zl[sT + NT * r];
+#pragma unroll
+            for (int r = 1; r < 16; r++) a[r] = cmul(a[r], twl[(r - 1) * 16 + x15]);
+            dft16<-1>(a, v);
+        }
+        __syncthreads();
+        {
+            const int b1 = (t >> 4) * 256;
+#pragma unroll
+            for (int r = 0; r < 16; r++) zl[b1 + 16 * r + (x15 ^ r)] = v[r];
+        }
+        __syncthreads();
+        {
+            float2 a[16];
+#pragma unroll
+            for (int r = 0; r < 16; r++) a[r] = zl[sT + NT * r];
+            twiddle_rec16<-1>(a, fw1, fw4);
+            dft16<-1>(a, v);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < 16; r++) zl[sT + NT * r] = v[r];
+        __syncthreads();
+        // ---------------- shared split, in place: thread-owned pairs (k, 4096 - k) ----------------
+        for (int k0 = t; k0 <= HALF / 2; k0 += NT) {
+            const int k1 = (HALF - k0) & (HALF - 1);
+            const float2 z0 = zl[swz(k0)], z1 = zl[swz(k1)];
+            zl[swz(k0)] = split2(z0, z1, post8192[k0]);
+            if (k1 != k0) zl[swz(k1)] = split2(z1, z0, post8192[k1]);
+        }
+        __syncthreads();
+
+        // ---------------- channels, CG at a time ----------------
+        const int cbeg = chunk * CHUNK_P, cend = min(cbeg + CHUNK_P, nch);
+        for (int c0 = cbeg; c0 < cend; c0 += CG) {
+            // pass 0: bins tb + m (- N), m = t + 256 r; X2 x H/2; DFT-R0 -> slice
+#pragma unroll
+            for (int g = 0; g < CG; g++) {
+                const int c = min(c0 + g, cend - 1);   // idle slots redo the last channel, never stored
+                const int tb = tunebins[c];
+                float2 a[R0], u[R0];
+#pragma unroll
+                for (int r = 0; r < R0; r++) {
+                    const int m = t + NT * r;
+                    const int bin = tb + m - (NT * r >= N / 2 ? N : 0);
+                    const float2 val = cmul(zl[swz(bin & (HALF - 1))], hr[r]);
+                    a[r] = (unsigned)bin < (unsigned)HALF ? val : make_float2(0.f, 0.f);
+                }
+                if constexpr (R0 == 16) dft16<+1>(a, u);
+                else dft<R0, +1>(a, u);
+                float2 *sl = wi + g * N;
+                if constexpr (R0 == 16) {
+#pragma unroll
+                    for (int r = 0; r < 16; r++) sl[16 * t + (r ^ x15)] = u[r];
+                } else {
+#pragma unroll
+                    for (int r = 0; r < R0; r++) sl[swz(R0 * t + r)] = u[r];
+                }
+            }
+            __syncthreads();
+            // pass 1: radix 16, NS = R0, table twiddles W_{16 R0}^{(j % R0) r}
+            float2 *sl = wi + cb * N;
+            float2 u[16];
+            {
+                float2 a[16];
+#pragma unroll
+                for (int r = 0; r < 16; r++) a[r] = sl[swz(jb + NB * r)];
+#pragma unroll
+                for (int r = 1; r < 16; r++) a[r] = cmulc(a[r], twl[15 * 16 + (r - 1) * R0 + (jb % R0)]);
+                dft16<+1>(a, u);
+            }
+            __syncthreads();
+            {
+                const int base = (jb / R0) * (16 * R0) + (jb % R0);
+#pragma unroll
+                for (int r = 0; r < 16; r++) sl[swz(base + R0 * r)] = u[r];
+            }
+            __syncthreads();
+            // pass 2: radix 16, NS = N/16, recurrence twiddles W_N^{j r}; overlap-discard store
+            {
+                float2 a[16];
+#pragma unroll
+                for (int r = 0; r < 16; r++) a[r] = sl[swz(jb + NB * r)];
+                twiddle_rec16<+1>(a, iw1, iw4);
+                dft16<+1>(a, u);
+            }
+            const int c = c0 + cb;
+            if (c < cend) {
+                const int fbase = blk * 8 * N + (k == 0 ? -N / 4 : N / 2 + (3 * N / 4) * (k - 1));
+                const __amdgpu_buffer_rsrc_t ro =
+                    buf_rsrc(static_cast<char *>(out) + ((size_t)c * stride + (size_t)fbase) * out_bytes<CS16>());
+                const int r0 = k == 0 ? 4 : 0;
+#pragma unroll
+                for (int r = 0; r < 12; r++) {
+                    if (r < r0) continue;
+                    store_iq<CS16>(flip(u[r], oa.lsbmask), ro, (unsigned)jb, (unsigned)(NB * r), oa);
+                }
+            }
+            __syncthreads();   // the slices are rewritten by the next group
+        }
+    }
+}
+
 int g_occ[3][8] = {};
+int g_occ_p[4][4] = {};
 int g_cus = 0;
 
 struct ChLaunch {
@@ -337,7 +511,51 @@ hipError_t launch_d(const KernelTables &t, const ChLaunch &L, int rand, int cs16
     return cs16 ? launch_c<D, false, true>(t, L) : launch_c<D, false, false>(t, L);
 }
 
+template <int D, bool RAND, bool CS16>
+hipError_t launch_p(const KernelTables &t, const ChLaunch &L)
+{
+    auto kern = r2iq_channels_p_kernel<D, RAND, CS16>;
+    int &occ = g_occ_p[D][(RAND ? 2 : 0) + (CS16 ? 1 : 0)];
+    if (occ == 0) {
+        int nb = 0;
+        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, NT, 0);
+        if (e != hipSuccess) return e;
+        e = hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, L.device);
+        if (e != hipSuccess) return e;
+        occ = nb > 0 ? nb : 1;
+    }
+    const int nframes = L.nblk * FRAMES;
+    const long long items = (long long)nframes * ((L.nch + CHUNK_P - 1) / CHUNK_P);
+    const int grid = (int)(items < (long long)g_cus * occ ? items : (long long)g_cus * occ);
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), 0, L.s, reinterpret_cast<const int *>(L.d_in), L.d_out,
+                       L.stride / 2, nframes, L.d_tunebins, L.nch, t.tw_p1, t.tw_q1[D], t.rec_f, t.rec_i[D],
+                       t.post8192, t.hsel[D], L.oa);
+    return hipGetLastError();
+}
+
+template <int D>
+hipError_t launch_pd(const KernelTables &t, const ChLaunch &L, int rand, int cs16)
+{
+    if (rand) return cs16 ? launch_p<D, true, true>(t, L) : launch_p<D, true, false>(t, L);
+    return cs16 ? launch_p<D, false, true>(t, L) : launch_p<D, false, false>(t, L);
+}
+
 }  // namespace
+
+hipError_t launch_channels_p(const KernelTables &t, int d, const int16_t *d_in, int nblk, const int *d_tunebins,
+                             int nch, void *d_out, size_t stride, int lsb, int rand, int cs16, float cs16_scale,
+                             int device, hipStream_t s)
+{
+    const ChLaunch L{d_in, nblk, d_tunebins, nch, d_out, stride, OutArgs{lsb ? 0x80000000u : 0u, cs16_scale},
+                     nullptr, device, s};
+    switch (d) {
+    case 0: return launch_pd<0>(t, L, rand, cs16);
+    case 1: return launch_pd<1>(t, L, rand, cs16);
+    case 2: return launch_pd<2>(t, L, rand, cs16);
+    case 3: return launch_pd<3>(t, L, rand, cs16);
+    default: return hipErrorInvalidValue;
+    }
+}
 
 bool channel_windows(int d, const int *tunebins, int nch, int2 *windows)
 {

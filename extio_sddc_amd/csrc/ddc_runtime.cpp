@@ -574,6 +574,9 @@ int sddc_ddc_process_channels_device(sddc_ddc_t *h, const int16_t *d_in, int nbl
     if (v2)
         HIP_TRY(sddc::launch_channels_v2(h->tables, h->d, d_in, nblk, h->d_tunebins, nch, d_out, out_stride,
                                          h->lsb, h->rand, cs16, h->cs16_scale, windows, h->device, s));
+    else if (h->variant != 1)
+        HIP_TRY(sddc::launch_channels_p(h->tables, h->d, d_in, nblk, h->d_tunebins, nch, d_out, out_stride,
+                                        h->lsb, h->rand, cs16, h->cs16_scale, h->device, s));
     else
         HIP_TRY(sddc::launch_channels(h->tables, h->d, d_in, nblk, h->d_tunebins, nch, d_out, out_stride,
                                       h->lsb, h->rand, cs16, h->cs16_scale, s));

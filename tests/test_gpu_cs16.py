@@ -104,7 +104,7 @@ def test_cs16_with_fine_tune(torch_dev):
     np.testing.assert_array_equal(c, to_cs16(y, scale))
 
 
-@pytest.mark.parametrize("d", [1, 4])      # v1 channels kernel (d < 4) and v2 (d >= 4)
+@pytest.mark.parametrize("d", [0, 3, 4])   # channels kernel for d < 4 (2^d channels in flight) and v2 (d >= 4)
 def test_channels_cs16_bit_exact(torch_dev, d):
     torch = torch_dev
     from extio_sddc_amd import output_samples

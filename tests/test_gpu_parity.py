@@ -174,7 +174,7 @@ def test_linearity_full_size(torch_dev, ddc):
     assert err.item() <= TOL
 
 
-@pytest.mark.parametrize("d", [0, 1, 4])
+@pytest.mark.parametrize("d", [0, 1, 2, 3, 4, 5, 6])
 def test_channels_match_single_channel(torch_dev, ddc, oracle, H, d):
     torch = torch_dev
     from extio_sddc_amd import output_samples

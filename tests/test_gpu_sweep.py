@@ -76,3 +76,51 @@ def test_random_config_parity(ddc, oracle, H, d, tb, lsb, rand, src, nblk, seed)
         assert np.all(np.isfinite(y))
         err = oracle.max_rel_err(y, r)
         assert err <= bar, f"variant {variant}: max-rel-err {err:.3e} (bar {bar:.3e})"
+
+
+def _channel_cases(seed=0x5DDC + 1):
+    """One case per d (0..6) plus one random d: channel counts across the 32-channel chunks of
+    the d < 4 kernel and the 128-channel chunks of the d >= 4 kernel, groups of 2^d channels
+    with idle slots, random (repeatable) tune bins, sideband and rand."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for d in list(range(7)) + [int(rng.integers(0, 7))]:
+        nch = int(rng.integers(1, 81)) if d < 4 else int(rng.integers(1, 300))
+        out.append((d, nch, int(rng.integers(0, 2)), int(rng.integers(0, 2)),
+                    ["mix", "uniform"][int(rng.integers(0, 2))], int(rng.integers(1, 1 << 30))))
+    return out
+
+
+@pytest.mark.parametrize("d,nch,lsb,rand,src,seed", _channel_cases())
+def test_random_channels(ddc, oracle, H, d, nch, lsb, rand, src, seed):
+    """Many-channel kernels (d < 4: r2iq_channels_p_kernel; d >= 4: r2iq_channels_v2_kernel) on
+    random tune-bin sets: every channel within 1e-5 of the single-channel kernel on the same
+    stream, and three random channels within 1e-5 of the f64 oracle.  Broadband sources only,
+    so no channel is leakage-only (see the module docstring)."""
+    import torch
+    from extio_sddc_amd import output_samples
+    rng = np.random.default_rng(seed)
+    nblk = 2
+    tbs = [4 * int(v) for v in rng.integers(0, 1024, nch)]
+    x = make_stream(nblk, src, seed=seed)
+    d_in = torch.from_numpy(x).to("cuda")
+    ddc.setDecimate(d)
+    ddc.setSideband(bool(lsb))
+    ddc.updateRand(bool(rand))
+    per = output_samples(d, nblk) * 2
+    out = torch.full((nch, per), float("nan"), dtype=torch.float32, device="cuda")
+    ddc.process_channels_device(d_in, nblk, tbs, out)
+    single = torch.empty(per, dtype=torch.float32, device="cuda")
+    worst = 0.0
+    for c in range(nch):
+        ddc.setTuneBin(tbs[c])
+        ddc.process_device(d_in, nblk, single)
+        torch.cuda.synchronize()
+        worst = max(worst, ((out[c] - single).abs().max() / single.abs().max()).item())
+    assert torch.isfinite(out).all()
+    assert worst <= TOL, f"channels vs single: {worst:.3e}"
+    y = out.cpu().numpy()
+    for c in rng.choice(nch, size=min(3, nch), replace=False):
+        r = oracle.r2iq(x, nblk, d, tbs[c], lsb, rand, H=H)
+        err = oracle.max_rel_err(y[c].view(np.complex64), r)
+        assert err <= TOL, f"channel {c} tb {tbs[c]}: {err:.3e}"
