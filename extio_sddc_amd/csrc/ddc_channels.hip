@@ -109,7 +109,7 @@ __global__ __launch_bounds__(NT, 2) void r2iq_channels_v2_kernel(
     const int *__restrict__ in32, void *__restrict__ out, size_t stride, int nframes,
     const int *__restrict__ tunebins, int nch, const float2 *__restrict__ tw_p1,
     const float2 *__restrict__ rec_f, const float2 *__restrict__ post8192, const float2 *__restrict__ hsel,
-    OutArgs oa, const int2 *__restrict__ windows)
+    OutArgs oa, const int2 *__restrict__ windows, float2 *__restrict__ scratch)
 {
     constexpr int N = HALF >> D;
     static_assert(N <= 256 && N >= 64, "channels v2 covers d = 4..6");
@@ -130,6 +130,12 @@ __global__ __launch_bounds__(NT, 2) void r2iq_channels_v2_kernel(
     const long long items = (long long)nframes * nchunks;
     const int i0 = (int)(items * blockIdx.x / gridDim.x), i1 = (int)(items * (blockIdx.x + 1) / gridDim.x);
     if (i0 >= i1) return;
+    // COMPACT with several chunks per frame: the frame's full X2 goes to this workgroup's
+    // scratch row once, and the frame's later chunks (the next items of the contiguous range)
+    // fill their windows from it instead of redoing the forward transform
+    const bool reuse = COMPACT && scratch != nullptr && nchunks > 1;   // uniform
+    float2 *const scr = reuse ? scratch + (size_t)blockIdx.x * HALF : nullptr;
+    int zf = -1;
     for (int i = tid; i < 15 * 16; i += NT) twl[i] = tw_p1[i];
     const float2 fw1_ = rec_f[tid], fw4_ = rec_f[NT + tid];
     const int l_ = tid % TPC, g_ = tid / TPC;
@@ -146,6 +152,9 @@ __global__ __launch_bounds__(NT, 2) void r2iq_channels_v2_kernel(
         const int f = it / nchunks, chunk = it - f * nchunks;
         const int blk = f / FRAMES, k = f - blk * FRAMES;
         const int sT = swz(t), x15 = t & 15;
+        const bool fresh = !reuse || f != zf;
+        if (fresh) {
+        zf = f;
         // ---------------- forward: Z = FFT4096(x_even + i x_odd) in zl ----------------
         float2 v[16];
         {
@@ -188,6 +197,24 @@ __global__ __launch_bounds__(NT, 2) void r2iq_channels_v2_kernel(
 #pragma unroll
         for (int r = 0; r < 16; r++) zl[sT + NT * r] = v[r];
         __syncthreads();
+        if (!COMPACT || reuse) {
+            // in place over all bins: thread-owned pairs (k, 4096 - k)
+            for (int k0 = t; k0 <= HALF / 2; k0 += NT) {
+                const int k1 = (HALF - k0) & (HALF - 1);
+                const float2 z0 = zl[swz(k0)], z1 = zl[swz(k1)];
+                const float2 x0 = split2(z0, z1, post8192[k0]), x1 = split2(z1, z0, post8192[k1]);
+                zl[swz(k0)] = x0;
+                if (k1 != k0) zl[swz(k1)] = x1;
+                if (reuse) {
+                    scr[k0] = x0;
+                    if (k1 != k0) scr[k1] = x1;
+                }
+            }
+            __syncthreads();
+        }
+        } else {
+            __syncthreads();   // the previous item's readers of xw are done
+        }
         int lo = 0;
         if constexpr (COMPACT) {
             // X2 of bins [lo, lo + w1) of this chunk's channels at xw[N/2 + bin - lo]
@@ -197,19 +224,14 @@ __global__ __launch_bounds__(NT, 2) void r2iq_channels_v2_kernel(
             for (int i = t; i < w1 + N; i += NT) {
                 const int bin = lo + i - N / 2;
                 float2 x2 = make_float2(0.f, 0.f);
-                if (i >= N / 2 && i < N / 2 + w1) x2 = split2(zl[swz(bin)], zl[swz((HALF - bin) & (HALF - 1))], post8192[bin]);
+                if (i >= N / 2 && i < N / 2 + w1) {
+                    if (!reuse) x2 = split2(zl[swz(bin)], zl[swz((HALF - bin) & (HALF - 1))], post8192[bin]);
+                    else if (fresh) x2 = zl[swz(bin)];
+                    else x2 = scr[bin];   // written by this workgroup before an earlier __syncthreads
+                }
                 xw[i] = x2;
             }
             __syncthreads();   // zl is overwritten by the channel slices from here on
-        } else {
-            // in place over all bins: thread-owned pairs (k, 4096 - k)
-            for (int k0 = t; k0 <= HALF / 2; k0 += NT) {
-                const int k1 = (HALF - k0) & (HALF - 1);
-                const float2 z0 = zl[swz(k0)], z1 = zl[swz(k1)];
-                zl[swz(k0)] = split2(z0, z1, post8192[k0]);
-                if (k1 != k0) zl[swz(k1)] = split2(z1, z0, post8192[k1]);
-            }
-            __syncthreads();
         }
 
         // ---------------- channels, G at a time ----------------
@@ -289,8 +311,9 @@ __global__ __launch_bounds__(NT, 2) void r2iq_channels_v2_kernel(
 
 // ---------------------------------------------------------------------------------------
 // Many channels at d = 0..3 (N = 4096 >> d >= 512): persistent, work item = (frame, chunk of
-// <= CHUNK_P channels).  Per item the forward transform (as ddc_persistent.hip) and the
-// shared r2c split X2 in place over all bins (buffer zl), then the channels CG = 2^d at a
+// <= CHUNK_P channels).  Per frame the forward transform (as ddc_persistent.hip) and the
+// shared r2c split X2 in place over all bins (buffer zl, kept for the frame's next chunks in
+// the workgroup's contiguous item range); per item the channels CG = 2^d at a
 // time, so every inverse pass keeps all 256 threads busy with 16 points each:
 //   pass 0  radix N/256 per channel (each thread: CG channels x N/256 bins; the filter taps of
 //           its bins live in registers), into the channels' N-element slices of `wi`
@@ -328,6 +351,7 @@ __global__ __launch_bounds__(NT, 2) void r2iq_channels_p_kernel(
 #pragma unroll
     for (int r = 0; r < R0; r++) hr[r] = hsel[tid + NT * r];
 
+    int zf = -1;   // frame whose split spectrum X2 is in zl (consecutive chunks of a frame reuse it)
     for (int it = i0; it < i1; it++) {
         int z = 0;
         asm volatile("" : "+s"(z));
@@ -337,6 +361,8 @@ __global__ __launch_bounds__(NT, 2) void r2iq_channels_p_kernel(
         const int f = it / nchunks, chunk = it - f * nchunks;
         const int blk = f / FRAMES, k = f - blk * FRAMES;
         const int sT = swz(t), x15 = t & 15;
+        if (f != zf) {   // workgroup-uniform
+        zf = f;
         // ---------------- forward: Z = FFT4096(x_even + i x_odd) in zl ----------------
         float2 v[16];
         {
@@ -387,6 +413,7 @@ __global__ __launch_bounds__(NT, 2) void r2iq_channels_p_kernel(
             if (k1 != k0) zl[swz(k1)] = split2(z1, z0, post8192[k1]);
         }
         __syncthreads();
+        }
 
         // ---------------- channels, CG at a time ----------------
         const int cbeg = chunk * CHUNK_P, cend = min(cbeg + CHUNK_P, nch);
@@ -472,6 +499,8 @@ struct ChLaunch {
     size_t stride;
     OutArgs oa;
     const int2 *windows;   // per-chunk compact windows, or nullptr
+    float2 *scratch;       // v2 COMPACT: per-workgroup X2 rows (scratch_rows x 4096), or nullptr
+    int scratch_rows;
     int device;
     hipStream_t s;
 };
@@ -492,9 +521,10 @@ hipError_t launch_v(const KernelTables &t, const ChLaunch &L)
     const int nframes = L.nblk * FRAMES;
     const long long items = (long long)nframes * ((L.nch + CHUNK - 1) / CHUNK);
     const int grid = (int)(items < (long long)g_cus * occ ? items : (long long)g_cus * occ);
+    float2 *scratch = grid <= L.scratch_rows ? L.scratch : nullptr;
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), 0, L.s, reinterpret_cast<const int *>(L.d_in), L.d_out,
                        L.stride / 2, nframes, L.d_tunebins, L.nch, t.tw_p1, t.rec_f, t.post8192, t.hsel[D], L.oa,
-                       L.windows);
+                       L.windows, scratch);
     return hipGetLastError();
 }
 
@@ -547,7 +577,7 @@ hipError_t launch_channels_p(const KernelTables &t, int d, const int16_t *d_in, 
                              int device, hipStream_t s)
 {
     const ChLaunch L{d_in, nblk, d_tunebins, nch, d_out, stride, OutArgs{lsb ? 0x80000000u : 0u, cs16_scale},
-                     nullptr, device, s};
+                     nullptr, nullptr, 0, device, s};
     switch (d) {
     case 0: return launch_pd<0>(t, L, rand, cs16);
     case 1: return launch_pd<1>(t, L, rand, cs16);
@@ -575,10 +605,11 @@ bool channel_windows(int d, const int *tunebins, int nch, int2 *windows)
 
 hipError_t launch_channels_v2(const KernelTables &t, int d, const int16_t *d_in, int nblk, const int *d_tunebins,
                               int nch, void *d_out, size_t stride, int lsb, int rand, int cs16, float cs16_scale,
-                              const int2 *d_windows, int device, hipStream_t s)
+                              const int2 *d_windows, float2 *d_scratch, int scratch_rows, int device,
+                              hipStream_t s)
 {
     const ChLaunch L{d_in, nblk, d_tunebins, nch, d_out, stride, OutArgs{lsb ? 0x80000000u : 0u, cs16_scale},
-                     d_windows, device, s};
+                     d_windows, d_scratch, scratch_rows, device, s};
     switch (d) {
     case 4: return launch_d<4>(t, L, rand, cs16);
     case 5: return launch_d<5>(t, L, rand, cs16);

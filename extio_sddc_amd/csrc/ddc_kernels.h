@@ -61,9 +61,12 @@ int channels_per_group(int d, int nch);
 // many-channel v2 (d = 4..6): persistent, forward once per (frame, 128-channel chunk)
 // stride: scalar components (float or int16) per channel row; cs16 as above.  d_windows:
 // per-128-channel-chunk forward-bin windows from channel_windows (device copy), or nullptr.
+// d_scratch: scratch_rows x 4096 float2, one row per workgroup, where a frame's split spectrum
+// is kept for its later chunks (used when the grid fits; nullptr = recompute per chunk).
 hipError_t launch_channels_v2(const KernelTables &t, int d, const int16_t *d_in, int nblk, const int *d_tunebins,
                               int nch, void *d_out, size_t stride, int lsb, int rand, int cs16, float cs16_scale,
-                              const int2 *d_windows, int device, hipStream_t s);
+                              const int2 *d_windows, float2 *d_scratch, int scratch_rows, int device,
+                              hipStream_t s);
 // many-channel, d = 0..3: persistent, forward + split once per (frame, 32-channel chunk), 2^d
 // channels' inverses in flight
 hipError_t launch_channels_p(const KernelTables &t, int d, const int16_t *d_in, int nblk, const int *d_tunebins,

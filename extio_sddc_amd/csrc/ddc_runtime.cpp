@@ -106,6 +106,8 @@ struct sddc_ddc {
     std::vector<int> tunebins_cached;
     int2 *d_windows = nullptr;             // per-chunk compact forward-bin windows (channels v2)
     int windows_d = -1;                    // d they were computed for; -2 = do not fit
+    float2 *d_chscratch = nullptr;         // channels v2: per-workgroup split-spectrum rows
+    int chscratch_rows = 0;
     hipStream_t ch_stream = nullptr;       // stream of the last many-channel launch
 
     // split x filter coefficients of the current (d, tunebin), rebuilt on device when either
@@ -295,6 +297,7 @@ int sddc_ddc_destroy(sddc_ddc_t *h)
         for (auto &r : h->regions) (void)hipHostUnregister(const_cast<char *>(r.first));
         if (h->d_tunebins) (void)hipFree(h->d_tunebins);
         if (h->d_windows) (void)hipFree(h->d_windows);
+        if (h->d_chscratch) (void)hipFree(h->d_chscratch);
         if (h->d_pq) (void)hipFree(h->d_pq);
         if (h->d_wave) (void)hipFree(h->d_wave);
         if (h->pq_used) (void)hipEventDestroy(h->pq_used);
@@ -570,10 +573,20 @@ int sddc_ddc_process_channels_device(sddc_ddc_t *h, const int16_t *d_in, int nbl
         }
         if (h->windows_d == h->d) windows = h->d_windows;
     }
+    if (v2 && windows && nch > 128 && !h->d_chscratch) {
+        // one 4096-bin row per resident workgroup (<= 4 per CU), 32 KB each
+        int cus = 0;
+        HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device));
+        HIP_TRY(hipMalloc(&h->d_chscratch, (size_t)cus * 4 * SDDC_DDC_HALF_FFT * sizeof(float2)));
+        h->chscratch_rows = cus * 4;
+    }
+    // the scratch rows are per handle: a launch on another stream must not overlap the last one
+    if (v2 && h->d_chscratch && h->ch_stream && h->ch_stream != s) HIP_TRY(hipStreamSynchronize(h->ch_stream));
     h->ch_stream = s;
     if (v2)
         HIP_TRY(sddc::launch_channels_v2(h->tables, h->d, d_in, nblk, h->d_tunebins, nch, d_out, out_stride,
-                                         h->lsb, h->rand, cs16, h->cs16_scale, windows, h->device, s));
+                                         h->lsb, h->rand, cs16, h->cs16_scale, windows, h->d_chscratch,
+                                         h->chscratch_rows, h->device, s));
     else if (h->variant != 1)
         HIP_TRY(sddc::launch_channels_p(h->tables, h->d, d_in, nblk, h->d_tunebins, nch, d_out, out_stride,
                                         h->lsb, h->rand, cs16, h->cs16_scale, h->device, s));
