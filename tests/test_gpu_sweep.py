@@ -1,4 +1,4 @@
-"""Seeded random parity sweep on a real MI355X (pytest -m gpu): 24 configurations drawn from
+"""Seeded random parity sweep on a real MI355X (pytest -m gpu): 48 configurations drawn from
 d in 0..6, any legal tune bin (multiple of 4, the setFreqOffset grid, fft_mt_r2iq.cpp:104),
 sideband, rand, the synthetic sources and 1..5 blocks, each checked against the f64 oracle.
 At d = 0 the wave kernel (variant 3) and the two-frame pipelined kernel (variant 4) are checked
@@ -25,7 +25,7 @@ TOL = 1e-5
 SOURCES = ["mix", "uniform", "bench", "oob"]
 
 
-def _cases(n=24, seed=0x5DDC):
+def _cases(n=48, seed=0x5DDC):
     rng = np.random.default_rng(seed)
     out = []
     for i in range(n):
@@ -79,12 +79,12 @@ def test_random_config_parity(ddc, oracle, H, d, tb, lsb, rand, src, nblk, seed)
 
 
 def _channel_cases(seed=0x5DDC + 1):
-    """One case per d (0..6) plus one random d: channel counts across the 32-channel chunks of
+    """Two cases per d (0..6) plus one random d: channel counts across the 32-channel chunks of
     the d < 4 kernel and the 128-channel chunks of the d >= 4 kernel, groups of 2^d channels
     with idle slots, random (repeatable) tune bins, sideband and rand."""
     rng = np.random.default_rng(seed)
     out = []
-    for d in list(range(7)) + [int(rng.integers(0, 7))]:
+    for d in list(range(7)) * 2 + [int(rng.integers(0, 7))]:
         nch = int(rng.integers(1, 81)) if d < 4 else int(rng.integers(1, 300))
         out.append((d, nch, int(rng.integers(0, 2)), int(rng.integers(0, 2)),
                     ["mix", "uniform"][int(rng.integers(0, 2))], int(rng.integers(1, 1 << 30))))
