@@ -322,20 +322,30 @@ __global__ __launch_bounds__(NT, 2) void r2iq_channels_v2_kernel(
 // 32 KB transform + 32 KB of channel slices + twiddles: 2 workgroups per CU.
 constexpr int CHUNK_P = 32;
 
-template <int D, bool RAND, bool CS16>
-__global__ __launch_bounds__(NT, 2) void r2iq_channels_p_kernel(
+#ifndef SDDC_CHP_WAVES
+#define SDDC_CHP_WAVES 3      // __launch_bounds__ min waves per SIMD of the L2X2 form
+#endif
+#ifndef SDDC_CHP_HREG
+#define SDDC_CHP_HREG 1       // filter taps of the pass-0 bins in registers (else loaded per channel)
+#endif
+template <int D, bool RAND, bool CS16, bool L2X2>
+__global__ __launch_bounds__(NT, L2X2 ? SDDC_CHP_WAVES : 2) void r2iq_channels_p_kernel(
     const int *__restrict__ in32, void *__restrict__ out, size_t stride, int nframes,
     const int *__restrict__ tunebins, int nch, const float2 *__restrict__ tw_p1, const float2 *__restrict__ tw_q1,
     const float2 *__restrict__ rec_f, const float2 *__restrict__ rec_i, const float2 *__restrict__ post8192,
-    const float2 *__restrict__ hsel, OutArgs oa)
+    const float2 *__restrict__ hsel, OutArgs oa, float2 *__restrict__ scratch)
 {
     constexpr int N = HALF >> D;
     static_assert(N >= 512, "d = 0..3");
     constexpr int R0 = N / 256;          // inverse pass-0 radix
     constexpr int NB = N / 16;           // radix-16 butterflies per channel in passes 1, 2
     constexpr int CG = NT / NB;          // channels in flight (2^d)
-    __shared__ __attribute__((aligned(16))) float2 zl[HALF];
+    // L2X2: the split spectrum goes to this workgroup's scratch row (L2-resident) instead of
+    // a second 32 KB of LDS, and the forward transform runs in the channel-slice buffer
+    __shared__ __attribute__((aligned(16))) float2 zbuf[L2X2 ? 1 : HALF];
     __shared__ __attribute__((aligned(16))) float2 wi[CG * N];
+    float2 *const zl = L2X2 ? wi : zbuf;
+    float2 *const scr = L2X2 ? scratch + (size_t)blockIdx.x * HALF : nullptr;
     __shared__ __attribute__((aligned(16))) float2 twl[15 * 16 + 15 * R0];
 
     const int tid = (int)threadIdx.x;
@@ -348,8 +358,10 @@ __global__ __launch_bounds__(NT, 2) void r2iq_channels_p_kernel(
     const int jb_ = tid % NB, cb_ = tid / NB;    // passes 1, 2: butterfly, channel in group
     const float2 iw1_ = rec_i[jb_], iw4_ = rec_i[NT + jb_];
     float2 hr[R0];   // H[m]/2 for this thread's pass-0 bins m = t + 256 r
+    if constexpr (SDDC_CHP_HREG || !L2X2) {
 #pragma unroll
-    for (int r = 0; r < R0; r++) hr[r] = hsel[tid + NT * r];
+        for (int r = 0; r < R0; r++) hr[r] = hsel[tid + NT * r];
+    }
 
     int zf = -1;   // frame whose split spectrum X2 is in zl (consecutive chunks of a frame reuse it)
     for (int it = i0; it < i1; it++) {
@@ -409,10 +421,16 @@ __global__ __launch_bounds__(NT, 2) void r2iq_channels_p_kernel(
         for (int k0 = t; k0 <= HALF / 2; k0 += NT) {
             const int k1 = (HALF - k0) & (HALF - 1);
             const float2 z0 = zl[swz(k0)], z1 = zl[swz(k1)];
-            zl[swz(k0)] = split2(z0, z1, post8192[k0]);
-            if (k1 != k0) zl[swz(k1)] = split2(z1, z0, post8192[k1]);
+            const float2 x0 = split2(z0, z1, post8192[k0]), x1 = split2(z1, z0, post8192[k1]);
+            if constexpr (L2X2) {
+                scr[k0] = x0;
+                if (k1 != k0) scr[k1] = x1;
+            } else {
+                zl[swz(k0)] = x0;
+                if (k1 != k0) zl[swz(k1)] = x1;
+            }
         }
-        __syncthreads();
+        __syncthreads();   // (L2X2: the scratch row is visible to the workgroup; wi is free)
         }
 
         // ---------------- channels, CG at a time ----------------
@@ -424,12 +442,28 @@ __global__ __launch_bounds__(NT, 2) void r2iq_channels_p_kernel(
                 const int c = min(c0 + g, cend - 1);   // idle slots redo the last channel, never stored
                 const int tb = tunebins[c];
                 float2 a[R0], u[R0];
+                if constexpr (L2X2) {
+                    const __amdgpu_buffer_rsrc_t rx = buf_rsrc(scr);
+                    float2 xv[R0], hv[R0];
 #pragma unroll
-                for (int r = 0; r < R0; r++) {
-                    const int m = t + NT * r;
-                    const int bin = tb + m - (NT * r >= N / 2 ? N : 0);
-                    const float2 val = cmul(zl[swz(bin & (HALF - 1))], hr[r]);
-                    a[r] = (unsigned)bin < (unsigned)HALF ? val : make_float2(0.f, 0.f);
+                    for (int r = 0; r < R0; r++) {
+                        const int bin = tb + t + NT * r - (NT * r >= N / 2 ? N : 0);
+                        xv[r] = buf_load8(rx, 8u * (unsigned)(bin & (HALF - 1)), 0u);
+                        hv[r] = SDDC_CHP_HREG ? hr[r] : hsel[t + NT * r];
+                    }
+#pragma unroll
+                    for (int r = 0; r < R0; r++) {
+                        const int bin = tb + t + NT * r - (NT * r >= N / 2 ? N : 0);
+                        a[r] = (unsigned)bin < (unsigned)HALF ? cmul(xv[r], hv[r]) : make_float2(0.f, 0.f);
+                    }
+                } else {
+#pragma unroll
+                    for (int r = 0; r < R0; r++) {
+                        const int m = t + NT * r;
+                        const int bin = tb + m - (NT * r >= N / 2 ? N : 0);
+                        const float2 val = cmul(zl[swz(bin & (HALF - 1))], hr[r]);
+                        a[r] = (unsigned)bin < (unsigned)HALF ? val : make_float2(0.f, 0.f);
+                    }
                 }
                 if constexpr (R0 == 16) dft16<+1>(a, u);
                 else dft<R0, +1>(a, u);
@@ -487,7 +521,7 @@ __global__ __launch_bounds__(NT, 2) void r2iq_channels_p_kernel(
 }
 
 int g_occ[3][8] = {};
-int g_occ_p[4][4] = {};
+int g_occ_p[4][8] = {};
 int g_cus = 0;
 
 struct ChLaunch {
@@ -541,11 +575,11 @@ hipError_t launch_d(const KernelTables &t, const ChLaunch &L, int rand, int cs16
     return cs16 ? launch_c<D, false, true>(t, L) : launch_c<D, false, false>(t, L);
 }
 
-template <int D, bool RAND, bool CS16>
-hipError_t launch_p(const KernelTables &t, const ChLaunch &L)
+template <int D, bool RAND, bool CS16, bool L2X2>
+hipError_t launch_p2(const KernelTables &t, const ChLaunch &L)
 {
-    auto kern = r2iq_channels_p_kernel<D, RAND, CS16>;
-    int &occ = g_occ_p[D][(RAND ? 2 : 0) + (CS16 ? 1 : 0)];
+    auto kern = r2iq_channels_p_kernel<D, RAND, CS16, L2X2>;
+    int &occ = g_occ_p[D][(L2X2 ? 4 : 0) + (RAND ? 2 : 0) + (CS16 ? 1 : 0)];
     if (occ == 0) {
         int nb = 0;
         hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, NT, 0);
@@ -559,8 +593,30 @@ hipError_t launch_p(const KernelTables &t, const ChLaunch &L)
     const int grid = (int)(items < (long long)g_cus * occ ? items : (long long)g_cus * occ);
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), 0, L.s, reinterpret_cast<const int *>(L.d_in), L.d_out,
                        L.stride / 2, nframes, L.d_tunebins, L.nch, t.tw_p1, t.tw_q1[D], t.rec_f, t.rec_i[D],
-                       t.post8192, t.hsel[D], L.oa);
+                       t.post8192, t.hsel[D], L.oa, L.scratch);
     return hipGetLastError();
+}
+
+#ifndef SDDC_CHP_L2
+#define SDDC_CHP_L2 1         // d >= 1: the L2X2 form when the handle's scratch rows cover the grid
+#endif                        // (+8-16 % at d = 1..3; at d = 0 it needs > 168 VGPRs and is no faster,
+                              // profiles/r01/channels/ab_channels_lowd_l2.txt)
+template <int D, bool RAND, bool CS16>
+hipError_t launch_p(const KernelTables &t, const ChLaunch &L)
+{
+    // the grid is at most CUs x 4 resident workgroups; the scratch holds L.scratch_rows rows
+    if constexpr (SDDC_CHP_L2 && D >= 1) {
+        if (L.scratch) {
+            if (g_cus == 0) {
+                hipError_t e = hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, L.device);
+                if (e != hipSuccess) return e;
+            }
+            if (g_cus * 4 <= L.scratch_rows) return launch_p2<D, RAND, CS16, true>(t, L);
+        }
+    }
+    ChLaunch L0 = L;
+    L0.scratch = nullptr;
+    return launch_p2<D, RAND, CS16, false>(t, L0);
 }
 
 template <int D>
@@ -574,10 +630,10 @@ hipError_t launch_pd(const KernelTables &t, const ChLaunch &L, int rand, int cs1
 
 hipError_t launch_channels_p(const KernelTables &t, int d, const int16_t *d_in, int nblk, const int *d_tunebins,
                              int nch, void *d_out, size_t stride, int lsb, int rand, int cs16, float cs16_scale,
-                             int device, hipStream_t s)
+                             float2 *d_scratch, int scratch_rows, int device, hipStream_t s)
 {
     const ChLaunch L{d_in, nblk, d_tunebins, nch, d_out, stride, OutArgs{lsb ? 0x80000000u : 0u, cs16_scale},
-                     nullptr, nullptr, 0, device, s};
+                     nullptr, d_scratch, scratch_rows, device, s};
     switch (d) {
     case 0: return launch_pd<0>(t, L, rand, cs16);
     case 1: return launch_pd<1>(t, L, rand, cs16);

@@ -67,11 +67,12 @@ hipError_t launch_channels_v2(const KernelTables &t, int d, const int16_t *d_in,
                               int nch, void *d_out, size_t stride, int lsb, int rand, int cs16, float cs16_scale,
                               const int2 *d_windows, float2 *d_scratch, int scratch_rows, int device,
                               hipStream_t s);
-// many-channel, d = 0..3: persistent, forward + split once per (frame, 32-channel chunk), 2^d
-// channels' inverses in flight
+// many-channel, d = 0..3: persistent, forward + split once per frame, 2^d channels' inverses
+// in flight.  d_scratch (scratch_rows x 4096 float2, >= CUs x 4 rows) holds each workgroup's
+// split spectrum in L2 instead of LDS; nullptr keeps it in LDS.
 hipError_t launch_channels_p(const KernelTables &t, int d, const int16_t *d_in, int nblk, const int *d_tunebins,
                              int nch, void *d_out, size_t stride, int lsb, int rand, int cs16, float cs16_scale,
-                             int device, hipStream_t s);
+                             float2 *d_scratch, int scratch_rows, int device, hipStream_t s);
 // host: the compact windows of every chunk; false if a chunk's window does not fit
 bool channel_windows(int d, const int *tunebins, int nch, int2 *windows);
 

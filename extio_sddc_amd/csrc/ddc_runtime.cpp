@@ -573,7 +573,7 @@ int sddc_ddc_process_channels_device(sddc_ddc_t *h, const int16_t *d_in, int nbl
         }
         if (h->windows_d == h->d) windows = h->d_windows;
     }
-    if (v2 && windows && nch > 128 && !h->d_chscratch) {
+    if (((v2 && windows && nch > 128) || !v2) && h->variant != 1 && !h->d_chscratch) {
         // one 4096-bin row per resident workgroup (<= 4 per CU), 32 KB each
         int cus = 0;
         HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device));
@@ -581,7 +581,7 @@ int sddc_ddc_process_channels_device(sddc_ddc_t *h, const int16_t *d_in, int nbl
         h->chscratch_rows = cus * 4;
     }
     // the scratch rows are per handle: a launch on another stream must not overlap the last one
-    if (v2 && h->d_chscratch && h->ch_stream && h->ch_stream != s) HIP_TRY(hipStreamSynchronize(h->ch_stream));
+    if (h->d_chscratch && h->ch_stream && h->ch_stream != s) HIP_TRY(hipStreamSynchronize(h->ch_stream));
     h->ch_stream = s;
     if (v2)
         HIP_TRY(sddc::launch_channels_v2(h->tables, h->d, d_in, nblk, h->d_tunebins, nch, d_out, out_stride,
@@ -589,7 +589,8 @@ int sddc_ddc_process_channels_device(sddc_ddc_t *h, const int16_t *d_in, int nbl
                                          h->chscratch_rows, h->device, s));
     else if (h->variant != 1)
         HIP_TRY(sddc::launch_channels_p(h->tables, h->d, d_in, nblk, h->d_tunebins, nch, d_out, out_stride,
-                                        h->lsb, h->rand, cs16, h->cs16_scale, h->device, s));
+                                        h->lsb, h->rand, cs16, h->cs16_scale, h->d_chscratch, h->chscratch_rows,
+                                        h->device, s));
     else
         HIP_TRY(sddc::launch_channels(h->tables, h->d, d_in, nblk, h->d_tunebins, nch, d_out, out_stride,
                                       h->lsb, h->rand, cs16, h->cs16_scale, s));
