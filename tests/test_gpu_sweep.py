@@ -88,6 +88,8 @@ def _channel_cases(seed=0x5DDC + 1):
         nch = int(rng.integers(1, 81)) if d < 4 else int(rng.integers(1, 300))
         out.append((d, nch, int(rng.integers(0, 2)), int(rng.integers(0, 2)),
                     ["mix", "uniform"][int(rng.integers(0, 2))], int(rng.integers(1, 1 << 30))))
+    # fewer channels than one group in flight (2^d at d < 4), and exactly one 128-channel chunk + 1
+    out += [(3, 1, 0, 0, "mix", 7), (2, 3, 1, 1, "uniform", 8), (4, 129, 0, 1, "mix", 9)]
     return out
 
 
