@@ -319,7 +319,9 @@ __global__ __launch_bounds__(NT, 2) void r2iq_channels_v2_kernel(
 //           its bins live in registers), into the channels' N-element slices of `wi`
 //   pass 1  radix 16, NS = N/256: thread t -> channel t / (N/16), butterfly t % (N/16)
 //   pass 2  radix 16, NS = N/16, register-recurrence twiddles, overlap-discard store
-// 32 KB transform + 32 KB of channel slices + twiddles: 2 workgroups per CU.
+// d = 0: 32 KB transform + 32 KB of channel slices + twiddles, 2 workgroups per CU.
+// d >= 1 (L2X2): the split spectrum goes to the workgroup's scratch row in L2 instead and the
+// forward transform runs in the slice buffer: 36 KB of LDS, 3 workgroups per CU (VGPR-bound).
 constexpr int CHUNK_P = 32;
 
 #ifndef SDDC_CHP_WAVES
