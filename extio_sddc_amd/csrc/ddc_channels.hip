@@ -322,7 +322,10 @@ __global__ __launch_bounds__(NT, 2) void r2iq_channels_v2_kernel(
 // d = 0: 32 KB transform + 32 KB of channel slices + twiddles, 2 workgroups per CU.
 // d >= 1 (L2X2): the split spectrum goes to the workgroup's scratch row in L2 instead and the
 // forward transform runs in the slice buffer: 36 KB of LDS, 3 workgroups per CU (VGPR-bound).
-constexpr int CHUNK_P = 32;
+#ifndef SDDC_CHUNK_P
+#define SDDC_CHUNK_P 32       // channels per work item
+#endif
+constexpr int CHUNK_P = SDDC_CHUNK_P;
 
 #ifndef SDDC_CHP_WAVES
 #define SDDC_CHP_WAVES 3      // __launch_bounds__ min waves per SIMD of the L2X2 form
