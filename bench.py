@@ -149,6 +149,41 @@ def load_traffic(workload: str):
         return None
 
 
+# VALU issue ceiling: 4 SIMDs x 256 CUs, one wave64 VALU instruction per SIMD every 2 cycles
+# (MI355X_MICROARCH.md "Wave scheduling"), at the 2400 MHz max clock
+VALU_SIMDS = 1024
+VALU_CYCLES_PER_INST = 2.0
+CLOCK_HZ = 2.4e9
+VALU_PEAK_INST_PER_S = VALU_SIMDS * CLOCK_HZ / VALU_CYCLES_PER_INST
+
+
+def load_valu(workload: str):
+    """Per-launch VALU wave-instructions counted with rocprofv3 --pmc SQ_INSTS_VALU
+    (profiles/pmc_valu.json, tools/pmc_valu.py), if present."""
+    p = os.path.join(ROOT, "profiles", "pmc_valu.json")
+    try:
+        with open(p) as f:
+            return json.load(f).get(workload)
+    except Exception:
+        return None
+
+
+def compute_roofline(workload: str, kern_ms: float):
+    """The bound the d = 0 kernel actually sits on: VALU issue.  achieved =
+    counted VALU wave-instructions per launch / the launch's HIP-event time; peak = the chip's
+    wave-instruction issue rate.  None when the workload has no committed count."""
+    v = load_valu(workload)
+    if not v:
+        return None
+    n = float(v["valu_insts_per_launch"])
+    ach = n / (kern_ms * 1e-3)
+    return {"bound": "valu-issue", "achieved": ach, "peak": VALU_PEAK_INST_PER_S, "unit": "wave-instructions/s",
+            "frac": ach / VALU_PEAK_INST_PER_S, "valu_insts_per_launch": n,
+            "peak_basis": f"{VALU_SIMDS} SIMDs x {CLOCK_HZ / 1e9:.1f} GHz / {VALU_CYCLES_PER_INST:g} cycles per "
+                          "wave64 VALU instruction",
+            "source": v.get("source")}
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -156,6 +191,9 @@ def main() -> None:
     # launches run ~20 % slower; 50 + 100 steps of 2048 blocks take ~50 ms
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--warmup-ms", type=float, default=250.0,
+                    help="after --warmup steps, keep launching untimed steps until this much wall time "
+                         "has passed, so the timed steps run at steady-state clocks (DESIGN.md §5)")
     ap.add_argument("--d", "--decim-index", dest="d", type=int, default=0,
                     help="decimation index (0 = decim 2); use --decim-index under torchrun")
     ap.add_argument("--tunebin", type=int, default=1024)
@@ -239,7 +277,7 @@ def main() -> None:
             # i + 1's broadcast runs while batch i is processed (double-buffered input)
             from extio_sddc_amd.shard import pipelined_batches
             d_in2 = d_in.clone()
-            batches = pipelined_batches([d_in, d_in2], args.warmup + args.steps, src=0)
+            batches = pipelined_batches([d_in, d_in2], None, src=0)   # unbounded; closed after timing
 
             def step():
                 ddc.process_channels_device(next(batches), nblk, tbs, d_out, stream)
@@ -249,9 +287,28 @@ def main() -> None:
         samples_per_step_all = nblk * BLOCK          # one shared stream
         workload = f"channels d={d} nblk={nblk} nch={args.channels}" + (" cs16" if args.cs16 else "")
 
+    tw0 = time.perf_counter()
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    # time floor on the warm-up: the first ~10 ms of back-to-back launches run ~20 % slower
+    # while the clocks ramp, so a short --warmup alone would time the ramp, not the kernel
+    # (every rank runs the same number of extra steps: the ranks agree on stopping, so the
+    # channel mode's collectives stay matched)
+    extra = 0
+    while True:
+        done = (time.perf_counter() - tw0) * 1e3 >= args.warmup_ms
+        if world > 1:
+            flag = torch.tensor([1 if done else 0], dtype=torch.int32, device=dev if backend == "nccl" else "cpu")
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+            done = bool(flag.item())
+        if done:
+            break
+        for _ in range(10):
+            step()
+        extra += 10
+        torch.cuda.synchronize()
+    warmup_ms = (time.perf_counter() - tw0) * 1e3
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -267,6 +324,8 @@ def main() -> None:
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     kern_ms = ev0.elapsed_time(ev1) / args.steps          # per step on the launch stream
+    if args.mode == "channels" and world > 1:
+        batches.close()                                   # waits for the prefetched broadcast
     t = torch.tensor([wall, kern_ms], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -309,7 +368,8 @@ def main() -> None:
     result = {
         "metric": "input MSamples/s at decim=2 + achieved % HBM roofline, 1 GPU; IQ max-rel-err",
         "value": value, "unit": "input MSamples/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": wall * 1e3 / args.steps, "higher_is_better": True,
+        "warmup": args.warmup, "warmup_ms": warmup_ms, "warmup_extra_steps": extra,
+        "ms_per_step": wall * 1e3 / args.steps, "higher_is_better": True,
         "scaling": "weak" if args.mode == "single" else "strong",
         "vs_baseline": None, "dtype": "f32 (int16 in, " + ("int16 IQ out)" if args.cs16 else "complex64 out)"), "data": "synthetic",
         "config": {"workload": "single-channel DDC, 128 MS/s int16 in, decim=2, 1xMI355X"
@@ -326,7 +386,8 @@ def main() -> None:
                      "kernel": "r2iq_persistent_kernel" if args.mode == "single" else "r2iq_channels_kernel",
                      "kernel_ms_per_launch": kern_ms,
                      "algorithmic_bytes_per_launch": alg_bytes,
-                     "bytes_per_input_sample": algorithmic_bytes_per_sample(d, nch_local, out_bytes)},
+                     "bytes_per_input_sample": algorithmic_bytes_per_sample(d, nch_local, out_bytes),
+                     "compute": compute_roofline(workload, kern_ms)},
     }
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -596,6 +596,13 @@ hipError_t launch_p2(const KernelTables &t, const ChLaunch &L)
     const int nframes = L.nblk * FRAMES;
     const long long items = (long long)nframes * ((L.nch + CHUNK_P - 1) / CHUNK_P);
     const int grid = (int)(items < (long long)g_cus * occ ? items : (long long)g_cus * occ);
+    if constexpr (L2X2) {
+        if (grid > L.scratch_rows) {   // one scratch row per workgroup: more workgroups than rows -> LDS form
+            ChLaunch L0 = L;
+            L0.scratch = nullptr;
+            return launch_p2<D, RAND, CS16, false>(t, L0);
+        }
+    }
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), 0, L.s, reinterpret_cast<const int *>(L.d_in), L.d_out,
                        L.stride / 2, nframes, L.d_tunebins, L.nch, t.tw_p1, t.tw_q1[D], t.rec_f, t.rec_i[D],
                        t.post8192, t.hsel[D], L.oa, L.scratch);

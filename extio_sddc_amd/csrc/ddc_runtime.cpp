@@ -69,6 +69,55 @@ constexpr int kBlock = SDDC_DDC_BLOCK;
 constexpr int kHostChunk = 32;   // blocks per pipeline chunk on the host path
 constexpr size_t kOutBlockMax = (size_t)SDDC_DDC_OUT_BLOCK * 2 * sizeof(float);   // bytes, CF32 d = 0
 
+// The streams whose launches read a per-handle device table (the (P, Q) coefficients, the NCO
+// staging buffer, the channel tune bins, the channel scratch rows).  The C ABI accepts any
+// stream per call, so before a table is rewritten the writing stream waits for the last launch
+// of EVERY stream that may still read it, not only the most recent one.
+struct Readers {
+    std::vector<std::pair<hipStream_t, hipEvent_t>> v;
+
+    // after a launch on s that reads the tables
+    hipError_t record(hipStream_t s)
+    {
+        for (auto &p : v)
+            if (p.first == s) return hipEventRecord(p.second, s);
+        if (v.size() >= 16) {   // bound the set: wait for all, forget them
+            hipError_t e = sync();
+            if (e != hipSuccess) return e;
+            clear();
+        }
+        hipEvent_t ev = nullptr;
+        hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+        if (e != hipSuccess) return e;
+        v.emplace_back(s, ev);
+        return hipEventRecord(ev, s);
+    }
+    // stream s (about to rewrite a table) waits for every other reader's last launch
+    hipError_t order_before(hipStream_t s) const
+    {
+        for (const auto &p : v)
+            if (p.first != s) {
+                hipError_t e = hipStreamWaitEvent(s, p.second, 0);
+                if (e != hipSuccess) return e;
+            }
+        return hipSuccess;
+    }
+    // the host waits for every reader (before a synchronous copy or a free)
+    hipError_t sync() const
+    {
+        for (const auto &p : v) {
+            hipError_t e = hipEventSynchronize(p.second);
+            if (e != hipSuccess) return e;
+        }
+        return hipSuccess;
+    }
+    void clear()
+    {
+        for (auto &p : v) (void)hipEventDestroy(p.second);
+        v.clear();
+    }
+};
+
 }  // namespace
 
 struct sddc_ddc {
@@ -84,7 +133,7 @@ struct sddc_ddc {
     sddc::KernelTables tables;
     float2 *d_tables = nullptr;
 
-    std::mutex mu;                         // serialises the host path and buffer growth
+    mutable std::mutex mu;                 // serialises the host path and buffer growth
     hipStream_t stream = nullptr;          // host path: compute stream
 
     // host path pipeline (process_host / process_blocks): two chunk slots; H2D on s_in,
@@ -108,17 +157,16 @@ struct sddc_ddc {
     int windows_d = -1;                    // d they were computed for; -2 = do not fit
     float2 *d_chscratch = nullptr;         // channels v2: per-workgroup split-spectrum rows
     int chscratch_rows = 0;
-    hipStream_t ch_stream = nullptr;       // stream of the last many-channel launch
+    Readers ch_readers;                    // streams of many-channel launches (tune bins, windows, scratch)
 
     // split x filter coefficients of the current (d, tunebin), rebuilt on device when either
-    // changes; pq_used marks the last launch that read them (possibly on another stream)
+    // changes; readers = the streams of single-channel launches that read them (and d_nco)
     float4 *d_pq = nullptr;
     int pq_d = -1, pq_tb = -1;
     // the d = 0 wave kernel's per-tunebin tables: pqW (4096 float4) then twI (4096 float2)
     float4 *d_wave = nullptr;
     int wave_tb = -1;
-    hipEvent_t pq_used = nullptr;
-    hipStream_t pq_stream = nullptr;
+    Readers readers;
 
     // fused fine-tune NCO: host chain + per-launch [T | lane starts] staged through a
     // pinned 3-slot ring into d_nco (stream-ordered copy before each launch)
@@ -255,7 +303,6 @@ int sddc_ddc_create(float gain, int device, sddc_ddc_t **out)
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipMalloc(&h->d_pq, SDDC_DDC_HALF_FFT * sizeof(float4));
     if (e == hipSuccess) e = hipMalloc(&h->d_wave, 4096 * (sizeof(float4) + sizeof(float2)));
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&h->pq_used, hipEventDisableTiming);
     if (e != hipSuccess) {
         sddc_ddc_destroy(h);
         return fail(SDDC_ERR_HIP, "create: %s", hipGetErrorString(e));
@@ -300,7 +347,10 @@ int sddc_ddc_destroy(sddc_ddc_t *h)
         if (h->d_chscratch) (void)hipFree(h->d_chscratch);
         if (h->d_pq) (void)hipFree(h->d_pq);
         if (h->d_wave) (void)hipFree(h->d_wave);
-        if (h->pq_used) (void)hipEventDestroy(h->pq_used);
+        (void)h->readers.sync();
+        (void)h->ch_readers.sync();
+        h->readers.clear();
+        h->ch_readers.clear();
         for (int i = 0; i < sddc_ddc::kNcoSlots; i++) {
             if (h->h_nco[i]) (void)hipHostFree(h->h_nco[i]);
             if (h->nco_ev[i]) (void)hipEventDestroy(h->nco_ev[i]);
@@ -316,6 +366,7 @@ int sddc_ddc_set_decimation(sddc_ddc_t *h, int d)
 {
     if (!h) return fail(SDDC_ERR_ARG, "null handle");
     if (d < 0 || d >= SDDC_DDC_NDEC) return fail(SDDC_ERR_ARG, "decimation index %d outside 0..6", d);
+    std::lock_guard<std::mutex> lk(h->mu);
     h->d = d;
     return SDDC_OK;
 }
@@ -323,6 +374,7 @@ int sddc_ddc_set_decimation(sddc_ddc_t *h, int d)
 int sddc_ddc_set_sideband(sddc_ddc_t *h, int lsb)
 {
     if (!h) return fail(SDDC_ERR_ARG, "null handle");
+    std::lock_guard<std::mutex> lk(h->mu);
     h->lsb = lsb ? 1 : 0;
     return SDDC_OK;
 }
@@ -330,6 +382,7 @@ int sddc_ddc_set_sideband(sddc_ddc_t *h, int lsb)
 int sddc_ddc_set_rand(sddc_ddc_t *h, int rand)
 {
     if (!h) return fail(SDDC_ERR_ARG, "null handle");
+    std::lock_guard<std::mutex> lk(h->mu);
     h->rand = rand ? 1 : 0;
     return SDDC_OK;
 }
@@ -339,11 +392,17 @@ int sddc_ddc_set_tunebin(sddc_ddc_t *h, int tunebin)
     if (!h) return fail(SDDC_ERR_ARG, "null handle");
     if (tunebin < 0 || tunebin >= SDDC_DDC_HALF_FFT)
         return fail(SDDC_ERR_ARG, "tune bin %d outside [0,4096)", tunebin);
+    std::lock_guard<std::mutex> lk(h->mu);
     h->tunebin = tunebin;
     return SDDC_OK;
 }
 
-int sddc_ddc_get_tunebin(const sddc_ddc_t *h) { return h ? h->tunebin : -1; }
+int sddc_ddc_get_tunebin(const sddc_ddc_t *h)
+{
+    if (!h) return -1;
+    std::lock_guard<std::mutex> lk(h->mu);
+    return h->tunebin;
+}
 
 float sddc_ddc_set_freq_offset(sddc_ddc_t *h, float offset)
 {
@@ -354,8 +413,9 @@ float sddc_ddc_set_freq_offset(sddc_ddc_t *h, float offset)
     // fft_mt_r2iq.cpp:104-106
     int tb = (int)(offset * SDDC_DDC_HALF_FFT / 4) * 4;
     const float delta = ((float)tb / SDDC_DDC_HALF_FFT) - offset;
-    const float ret = delta * (float)(1 << h->d);
     tb = std::min(std::max(tb, 0), SDDC_DDC_HALF_FFT - 4);
+    std::lock_guard<std::mutex> lk(h->mu);
+    const float ret = delta * (float)(1 << h->d);
     h->tunebin = tb;
     return ret;
 }
@@ -390,15 +450,15 @@ static hipError_t stage_nco(sddc_ddc_t *h, int nblk, hipStream_t s)
         h->h_nco_cap = n;
     }
     if (n > h->d_nco_cap) {   // the previous launches may still read the old buffer
-        if (h->pq_stream && (e = hipStreamSynchronize(h->pq_stream)) != hipSuccess) return e;
+        if ((e = h->readers.sync()) != hipSuccess) return e;
         if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
         if (h->d_nco) (void)hipFree(h->d_nco);
         h->d_nco = nullptr;
         h->d_nco_cap = 0;
         if ((e = hipMalloc(&h->d_nco, n * sizeof(float2))) != hipSuccess) return e;
         h->d_nco_cap = n;
-    } else if (h->pq_stream && h->pq_stream != s) {   // a launch on another stream may still read d_nco
-        if ((e = hipStreamWaitEvent(s, h->pq_used, 0)) != hipSuccess) return e;
+    } else if ((e = h->readers.order_before(s)) != hipSuccess) {   // launches on other streams may still read d_nco
+        return e;
     }
     const int slot = h->nco_slot;
     h->nco_slot = (slot + 1) % sddc_ddc::kNcoSlots;
@@ -428,11 +488,9 @@ static hipError_t launch_single(sddc_ddc_t *h, const int16_t *d_in, int nblk, vo
         float4 *pqW = h->d_wave;
         float2 *twI = reinterpret_cast<float2 *>(h->d_wave + 4096);
         if (h->wave_tb != h->tunebin) {
-            if (h->pq_stream && h->pq_stream != s) {   // a launch on another stream may still read them
-                hipError_t e = hipStreamWaitEvent(s, h->pq_used, 0);
-                if (e != hipSuccess) return e;
-            }
-            hipError_t e = sddc::launch_build_wave_tables(h->tables, h->tunebin, pqW, twI, s);
+            hipError_t e = h->readers.order_before(s);   // launches on other streams may still read them
+            if (e != hipSuccess) return e;
+            e = sddc::launch_build_wave_tables(h->tables, h->tunebin, pqW, twI, s);
             if (e != hipSuccess) return e;
             h->wave_tb = h->tunebin;
         }
@@ -440,15 +498,12 @@ static hipError_t launch_single(sddc_ddc_t *h, const int16_t *d_in, int nblk, vo
             h->tables, d_in, nblk, d_out, pqW, twI, h->tunebin, h->lsb, h->rand, h->out_fmt == SDDC_DDC_FMT_CS16,
             h->cs16_scale, nco ? h->d_nco + sddc::FineTune::kTable : nullptr, nco ? h->d_nco : nullptr, h->device, s);
         if (e != hipSuccess) return e;
-        h->pq_stream = s;
-        return hipEventRecord(h->pq_used, s);
+        return h->readers.record(s);
     }
     if (h->pq_d != h->d || h->pq_tb != h->tunebin) {
-        if (h->pq_stream && h->pq_stream != s) {   // a launch on another stream may still read d_pq
-            hipError_t e = hipStreamWaitEvent(s, h->pq_used, 0);
-            if (e != hipSuccess) return e;
-        }
-        hipError_t e = sddc::launch_build_split_filter(h->tables, h->d, h->tunebin, h->d_pq, s);
+        hipError_t e = h->readers.order_before(s);   // launches on other streams may still read d_pq
+        if (e != hipSuccess) return e;
+        e = sddc::launch_build_split_filter(h->tables, h->d, h->tunebin, h->d_pq, s);
         if (e != hipSuccess) return e;
         h->pq_d = h->d;
         h->pq_tb = h->tunebin;
@@ -465,8 +520,7 @@ static hipError_t launch_single(sddc_ddc_t *h, const int16_t *d_in, int nblk, vo
                                          h->out_fmt == SDDC_DDC_FMT_CS16, h->cs16_scale, nco_starts, nco_trig,
                                          h->device, s);
     if (e != hipSuccess) return e;
-    h->pq_stream = s;
-    return hipEventRecord(h->pq_used, s);
+    return h->readers.record(s);
 }
 
 int sddc_ddc_set_output_format(sddc_ddc_t *h, int format, float cs16_scale)
@@ -498,6 +552,7 @@ int sddc_ddc_set_fine_tune(sddc_ddc_t *h, float relative_freq)
 int sddc_ddc_internal_set_variant(sddc_ddc_t *h, int variant)
 {
     if (!h || variant < 0 || variant > 5 || variant == 2) return fail(SDDC_ERR_ARG, "bad variant");
+    std::lock_guard<std::mutex> lk(h->mu);
     h->variant = variant;
     return SDDC_OK;
 }
@@ -516,9 +571,10 @@ static int check_process_args(sddc_ddc_t *h, const int16_t *in, int nblk, const 
 
 int sddc_ddc_process_device(sddc_ddc_t *h, const int16_t *d_in, int nblk, void *d_out, void *hip_stream)
 {
+    if (!h) return fail(SDDC_ERR_ARG, "null handle");
+    std::lock_guard<std::mutex> lk(h->mu);   // the call reads d, format, tune bin: one consistent set
     int rc = check_process_args(h, d_in, nblk, d_out);
     if (rc) return rc;
-    std::lock_guard<std::mutex> lk(h->mu);
     DeviceGuard g(h->device);
     HIP_TRY(g.err);
     HIP_TRY(launch_single(h, d_in, nblk, d_out, (hipStream_t)hip_stream));
@@ -528,6 +584,8 @@ int sddc_ddc_process_device(sddc_ddc_t *h, const int16_t *d_in, int nblk, void *
 int sddc_ddc_process_channels_device(sddc_ddc_t *h, const int16_t *d_in, int nblk, const int *tunebins,
                                      int nch, void *d_out, size_t out_stride, void *hip_stream)
 {
+    if (!h) return fail(SDDC_ERR_ARG, "null handle");
+    std::lock_guard<std::mutex> lk(h->mu);   // d, format and NCO state are read below
     int rc = check_process_args(h, d_in, nblk, d_out);
     if (rc) return rc;
     if (!tunebins || nch <= 0 || nch > SDDC_DDC_MAX_CHANNELS)
@@ -539,17 +597,18 @@ int sddc_ddc_process_channels_device(sddc_ddc_t *h, const int16_t *d_in, int nbl
     const size_t need = (size_t)nblk * (size_t)(SDDC_DDC_OUT_BLOCK >> h->d) * 2;
     if (nch > 1 && out_stride < need)
         return fail(SDDC_ERR_ARG, "out_stride %zu < %zu components per channel", out_stride, need);
+    if (nch > 1 && (out_stride & 1))   // channels start on whole complex samples
+        return fail(SDDC_ERR_ARG, "out_stride %zu must be even (components, 2 per complex sample)", out_stride);
     const int cs16 = h->out_fmt == SDDC_DDC_FMT_CS16;
     DeviceGuard g(h->device);
     HIP_TRY(g.err);
-    std::lock_guard<std::mutex> lk(h->mu);
     hipStream_t s = (hipStream_t)hip_stream;
     const bool v2 = h->d >= 4 && h->variant != 1;
     const bool changed = h->tunebins_cached.size() != (size_t)nch ||
                          !std::equal(h->tunebins_cached.begin(), h->tunebins_cached.end(), tunebins);
     if (changed || (v2 && h->windows_d != h->d && h->windows_d != -2 - 8 * h->d)) {
-        // earlier launches may still read the device copies
-        if (h->ch_stream) HIP_TRY(hipStreamSynchronize(h->ch_stream));
+        // earlier launches, on any stream, may still read the device copies
+        HIP_TRY(h->ch_readers.sync());
         HIP_TRY(hipStreamSynchronize(s));
     }
     if (changed) {
@@ -580,9 +639,8 @@ int sddc_ddc_process_channels_device(sddc_ddc_t *h, const int16_t *d_in, int nbl
         HIP_TRY(hipMalloc(&h->d_chscratch, (size_t)cus * 4 * SDDC_DDC_HALF_FFT * sizeof(float2)));
         h->chscratch_rows = cus * 4;
     }
-    // the scratch rows are per handle: a launch on another stream must not overlap the last one
-    if (h->d_chscratch && h->ch_stream && h->ch_stream != s) HIP_TRY(hipStreamSynchronize(h->ch_stream));
-    h->ch_stream = s;
+    // the scratch rows are per handle: a launch must not overlap one on another stream
+    if (h->d_chscratch) HIP_TRY(h->ch_readers.order_before(s));
     if (v2)
         HIP_TRY(sddc::launch_channels_v2(h->tables, h->d, d_in, nblk, h->d_tunebins, nch, d_out, out_stride,
                                          h->lsb, h->rand, cs16, h->cs16_scale, windows, h->d_chscratch,
@@ -594,6 +652,7 @@ int sddc_ddc_process_channels_device(sddc_ddc_t *h, const int16_t *d_in, int nbl
     else
         HIP_TRY(sddc::launch_channels(h->tables, h->d, d_in, nblk, h->d_tunebins, nch, d_out, out_stride,
                                       h->lsb, h->rand, cs16, h->cs16_scale, s));
+    HIP_TRY(h->ch_readers.record(s));
     return SDDC_OK;
 }
 
@@ -717,24 +776,26 @@ static int host_pipeline(sddc_ddc_t *h, int nblk, Src src, void *out)
 
 int sddc_ddc_process_host(sddc_ddc_t *h, const int16_t *in, int nblk, void *out)
 {
+    if (!h) return fail(SDDC_ERR_ARG, "null handle");
+    std::lock_guard<std::mutex> lk(h->mu);
     int rc = check_process_args(h, in, nblk, out);
     if (rc) return rc;
     DeviceGuard g(h->device);
     HIP_TRY(g.err);
-    std::lock_guard<std::mutex> lk(h->mu);
     return host_pipeline(h, nblk, [in](int i) { return in + (size_t)i * kBlock; }, out);
 }
 
 int sddc_ddc_process_blocks(sddc_ddc_t *h, const int16_t *const *blocks, int nblk, void *out)
 {
+    if (!h) return fail(SDDC_ERR_ARG, "null handle");
     if (!blocks) return fail(SDDC_ERR_ARG, "null block list");
+    std::lock_guard<std::mutex> lk(h->mu);
     int rc = check_process_args(h, nblk > 0 ? blocks[0] : nullptr, nblk, out);
     if (rc) return rc;
     for (int i = 0; i < nblk; i++)
         if (!blocks[i] || ((uintptr_t)blocks[i] & 3)) return fail(SDDC_ERR_ARG, "block %d null or unaligned", i);
     DeviceGuard g(h->device);
     HIP_TRY(g.err);
-    std::lock_guard<std::mutex> lk(h->mu);
     return host_pipeline(h, nblk, [blocks](int i) { return blocks[i]; }, out);
 }
 

@@ -15,6 +15,7 @@
 #include <cstdlib>
 #include <cstring>
 
+#include "batching.h"
 #include "sddc_ddc.h"
 
 // ---- ABI guard: the base class must be byte-identical to Core/r2iq.h ----------------
@@ -183,15 +184,20 @@ void fft_mt_r2iq::worker()
             stage_cv_.wait(lk, [&] { return stage_n_[stage] == 0 || !r2iqOn; });
         }
         if (!r2iqOn) break;
-        const int tb = mtunebin.load();                  // per block, impl.hpp:20
-        const bool rnd = getRand();                      // per block, impl.hpp:40
         const int16_t *blocks[kMaxBatch];
         blocks[0] = inputbuffer->getReadPtr();           // blocks while empty
         if (!r2iqOn) break;
+        // Tune bin and rand of each block are read as the worker takes that block, as the
+        // reference reads them once per block (impl.hpp:20, 40).  One GPU call runs one
+        // (tunebin, rand) pair, so a block whose values differ from the batch head's starts
+        // the next batch instead of joining this one.
+        const int tb = mtunebin.load();
+        const bool rnd = getRand();
         int n = 1;
         // take more blocks only if they are already queued (never wait for them); they stay
         // in the ring, read in place, until the GPU has copied them
-        while (n < kMaxBatch && (uint64_t)(inputbuffer->getWriteCount() - wc_base_) > consumed_ + n) {
+        while (n < kMaxBatch && sddc_r2iq::queued_blocks(inputbuffer->getWriteCount(), wc_base_, consumed_) > (uint32_t)n) {
+            if (mtunebin.load() != tb || getRand() != rnd) break;
             blocks[n] = inputbuffer->peekReadPtr(n);
             n++;
         }

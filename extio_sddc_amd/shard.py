@@ -44,6 +44,8 @@ def pipelined_batches(bufs, nbatches: int, src: int = 0, fill=None):
     rank's batch by broadcast, with the broadcast of batch i + 1 already in flight while the
     caller processes batch i (overlap the xGMI broadcast with the compute).
 
+    nbatches: None = unbounded (the caller stops with close(), which waits for the broadcast
+    already in flight, so every rank leaves with its collectives matched).
     bufs: two equal int16 buffers.  fill(buf, i): on the src rank, writes batch i into buf
     before it is sent (None: the buffers already hold the batch, as in bench.py).
     Ordering on a GPU: an async collective first waits for the work queued on the current
@@ -61,11 +63,18 @@ def pipelined_batches(bufs, nbatches: int, src: int = 0, fill=None):
             fill(b, i)
         return dist.broadcast(b.view(torch.int32), src=src, async_op=True)
 
-    if nbatches <= 0:
+    if nbatches is not None and nbatches <= 0:
         return
     work = send(0)
-    for i in range(nbatches):
-        work.wait()
-        if i + 1 < nbatches:
-            work = send(i + 1)
-        yield bufs[i % 2]
+    i = 0
+    try:
+        while nbatches is None or i < nbatches:
+            work.wait()
+            work = None
+            if nbatches is None or i + 1 < nbatches:
+                work = send(i + 1)
+            yield bufs[i % 2]
+            i += 1
+    finally:   # close(): the prefetched broadcast still completes on every rank
+        if work is not None:
+            work.wait()

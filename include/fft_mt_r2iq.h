@@ -11,8 +11,8 @@
  *   - Init(gain, in, out) designs the 7 filter banks (fft_mt_r2iq.cpp:147-227);
  *   - TurnOn() latches decimation and sideband, starts both rings and one worker
  *     (fft_mt_r2iq.cpp:111-129, impl.hpp:3-7); the history starts at zero;
- *   - updateRand() and setFreqOffset() take effect at the next input block
- *     (impl.hpp:20,40);
+ *   - updateRand() and setFreqOffset() take effect at the next input block the worker
+ *     takes (impl.hpp:20,40): both are read per block, and a batch is cut where they change;
  *   - each input block yields 32768>>d complex floats; one output ring block
  *     (EXT_BLOCKLEN = 32768 complex) is released every 2^d input blocks
  *     (impl.hpp:100-148);

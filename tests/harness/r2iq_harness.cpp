@@ -10,6 +10,10 @@
 // included); IN.bin may hold fewer blocks than NBLK, it is then cycled.  CYCLES > 1 repeats
 // TurnOn -> NBLK blocks -> TurnOff on the same object and rings (the Start/Stop cycling of
 // unittest/stability_test.cpp:255-301); each cycle's IQ is appended to OUT.bin.
+// Env R2IQ_SCHEDULE="K:TUNEBIN:RAND[,K:TUNEBIN:RAND...]" (first cycle): before writing input
+// block K the producer waits until the class has processed blocks 0..K-1, then calls
+// setFreqOffset(TUNEBIN/4096) and updateRand(RAND), so block K is the first to run with them
+// (the reference reads both once per block, Core/fft_mt_r2iq_impl.hpp:20,40).
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -41,6 +45,21 @@ int main(int argc, char **argv)
     if (fread(data.data(), sizeof(int16_t), data.size(), in) != data.size()) return 2;
     std::fclose(in);
     const bool discard = std::strcmp(argv[8], "-") == 0;
+    struct Change { int k, tb, rand; };
+    std::vector<Change> sched;
+    if (const char *e = std::getenv("R2IQ_SCHEDULE")) {
+        for (const char *p = e; *p;) {
+            Change c{};
+            int used = 0;
+            if (std::sscanf(p, "%d:%d:%d%n", &c.k, &c.tb, &c.rand, &used) != 3) {
+                std::fprintf(stderr, "bad R2IQ_SCHEDULE at '%s'\n", p);
+                return 2;
+            }
+            sched.push_back(c);
+            p += used;
+            if (*p == ',') p++;
+        }
+    }
 
     ringbuffer<int16_t> inbuf;           // 64 slots, like RadioHandlerClass::inputbuffer
     ringbuffer<float> outbuf;
@@ -70,6 +89,13 @@ int main(int argc, char **argv)
         }
         std::thread producer([&] {
             for (int b = 0; b < nblk; b++) {
+                for (const Change &c : sched) {
+                    if (cyc != 0 || c.k != b) continue;
+                    while (r.blocksProcessed() < (uint64_t)b && base->IsOn())
+                        std::this_thread::sleep_for(std::chrono::microseconds(200));
+                    base->setFreqOffset((float)c.tb / 4096.0f);
+                    base->updateRand(c.rand != 0);
+                }
                 int16_t *p = inbuf.getWritePtr();
                 if (!base->IsOn()) return;
                 std::memcpy(p, data.data() + (size_t)(b % have) * 65536, 65536 * sizeof(int16_t));

@@ -63,3 +63,35 @@ def test_reference_radiohandler_links_against_dropin():
 def test_standalone_harness_built():
     assert os.path.exists(os.path.join(ROOT, "build", "bin", "r2iq_harness")), \
         "run make -C extio_sddc_amd/csrc (or __graft_entry__.build())"
+
+
+def test_queued_blocks_survives_write_count_wrap(tmp_path):
+    """The worker's batching count (csrc/r2iq/batching.h) stays exact when the ring's int
+    writeCount (Core/dsp/ringbuffer.h, never reset) passes INT_MAX after 2^31 blocks."""
+    src = tmp_path / "t.cpp"
+    src.write_text(r'''
+#include <climits>
+#include <cstdio>
+#include <initializer_list>
+#include "batching.h"
+using sddc_r2iq::queued_blocks;
+static int wrap(long long v) { return (int)(unsigned)(v & 0xffffffffLL); }   // two's complement int
+int main() {
+    int bad = 0;
+    for (long long base : {0LL, (long long)INT_MAX - 5, (long long)INT_MAX, 4294967290LL}) {
+        for (long long consumed = 0; consumed < 40; consumed += 3)
+            for (long long queued = 0; queued < 20; queued++) {
+                const long long wc = base + consumed + queued;
+                if (queued_blocks(wrap(wc), wrap(base), (unsigned long long)consumed) != (unsigned)queued) bad++;
+            }
+    }
+    std::printf("%d\n", bad);
+    return bad != 0;
+}
+''')
+    exe = tmp_path / "t"
+    p = subprocess.run(["g++", "-std=c++17", "-O2", "-fwrapv", "-I", os.path.join(ROOT, "extio_sddc_amd", "csrc", "r2iq"),
+                        str(src), "-o", str(exe)], capture_output=True, text=True)
+    assert p.returncode == 0, p.stderr
+    r = subprocess.run([str(exe)], capture_output=True, text=True)
+    assert r.returncode == 0 and r.stdout.strip() == "0", r.stdout

@@ -26,8 +26,9 @@ TOL = 1e-5
 BBRF103_GAINFACTOR = np.float32(7.8e-8)   # DummyRadio's gain (Core/RadioHandler.h:143, config.h:57)
 
 
-def _run(cmd, timeout=120):
-    p = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout)
+def _run(cmd, timeout=120, env=None):
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout,
+                       env=dict(os.environ, SDDC_DDC_BACKEND="hip", **(env or {})))
     assert p.returncode == 0, f"{cmd[0]} rc={p.returncode}\n{p.stdout}\n{p.stderr}"
     return p.stdout
 
@@ -106,3 +107,30 @@ def test_dropin_start_stop_cycles(tmp_path, oracle):
     for c in range(cycles):
         assert oracle.max_rel_err(y[c], ref) <= TOL
         np.testing.assert_array_equal(y[c].view(np.uint32), y[0].view(np.uint32))
+
+
+@pytest.mark.parametrize("d,nblk,sched", [
+    (1, 8, [(3, 2048, 1), (6, 284, 0)]),            # tune and rand change mid-stream
+    (0, 9, [(1, 3888, 0), (2, 3888, 1), (5, 0, 1)]),   # rand alone, then tune alone, edge bins
+    (2, 12, [(4, 512, 0)]),                         # inside one output block (4 inputs per output)
+])
+def test_dropin_per_block_tune_and_rand(tmp_path, oracle, d, nblk, sched):
+    """setFreqOffset / updateRand between two known input blocks: the reference reads the tune
+    bin and rand once per block (Core/fft_mt_r2iq_impl.hpp:20, 40), so every block's IQ must be
+    the oracle's at THAT block's (tunebin, rand), even though the drop-in batches queued blocks
+    into one GPU call (a batch is cut where either value changes)."""
+    tb0, rand0 = 1024, 0
+    x = make_stream(nblk, "mix")
+    fin, fout = tmp_path / "in.bin", tmp_path / "out.bin"
+    x[4096:].tofile(fin)
+    spec = ",".join(f"{k}:{tb}:{r}" for k, tb, r in sched)
+    _run([HARNESS, str(fin), str(nblk), str(d), str(tb0), "0", str(rand0), "1.0", str(fout)],
+         env={"R2IQ_SCHEDULE": spec})
+    y = np.fromfile(fout, np.float32).view(np.complex64)
+    per = 32768 >> d
+    assert y.size == nblk * per
+    bounds = [(0, tb0, rand0)] + list(sched) + [(nblk, None, None)]
+    for (a, tb, r), (b, _, _) in zip(bounds[:-1], bounds[1:]):
+        seg = x[a * 65536: 4096 + b * 65536]          # blocks a..b-1 with their history
+        ref = oracle.r2iq(seg, b - a, d, tb, False, r)
+        assert oracle.max_rel_err(y[a * per: b * per], ref) <= TOL, (a, b, tb, r)
