@@ -73,6 +73,14 @@ CASES = [
     (5, 2048, 0, 1, "mix"),
     (6, 1024, 1, 0, "mix"),
     (6, 4, 0, 0, "uniform"),
+    # strong out-of-band tone + weak in-band tone at the BASELINE configs' tune bin (strict bar):
+    # C2 (d=0), the C3 decimation sweep (d=1..4) and C4 (d=1, lsb, rand)
+    (0, 1024, 0, 0, "oob"),
+    (1, 1024, 0, 0, "oob"),
+    (2, 1024, 0, 0, "oob"),
+    (3, 1024, 0, 0, "oob"),
+    (4, 1024, 0, 0, "oob"),
+    (1, 1024, 1, 1, "oob"),
 ]
 
 
@@ -194,30 +202,6 @@ def test_channels_match_single_channel(torch_dev, ddc, oracle, H, d):
         r = oracle.r2iq(x, nblk, d, tb, H=H)
         yc = y[c].view(np.complex64)
         assert oracle.max_rel_err(yc, r) <= TOL, f"channel {c} tb {tb}"
-
-
-def test_1024_channels_d4(torch_dev, ddc):
-    """C5 shape: all 1024 legal tune bins at d=4; spot-check against single-channel runs."""
-    torch = torch_dev
-    from extio_sddc_amd import output_samples
-    nblk, d = 2, 4
-    x = make_stream(nblk, "mix")
-    tbs = list(range(0, 4096, 4))
-    ddc.setDecimate(d)
-    ddc.setSideband(False)
-    ddc.updateRand(False)
-    d_in = torch.from_numpy(x).to("cuda")
-    per = output_samples(d, nblk) * 2
-    out = torch.full((1024, per), float("nan"), dtype=torch.float32, device="cuda")
-    ddc.process_channels_device(d_in, nblk, tbs, out)
-    single = torch.empty(per, dtype=torch.float32, device="cuda")
-    for c in (0, 1, 255, 256, 511, 700, 1023):
-        ddc.setTuneBin(tbs[c])
-        ddc.process_device(d_in, nblk, single)
-        torch.cuda.synchronize()
-        ref = single.abs().max()
-        assert ((out[c] - single).abs().max() / ref).item() <= TOL
-    assert torch.isfinite(out).all()
 
 
 def test_bad_arguments_raise(torch_dev, ddc):
