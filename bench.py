@@ -55,86 +55,154 @@ def make_input(torch, nblk: int, seed: int, device) -> "torch.Tensor":
     return out
 
 
-def cpu_baseline(d: int, tunebin: int, gpu_sample_out, sample_in: np.ndarray, nblk_sample: int,
-                 budget_s: float) -> dict:
-    """Time the oracle's float32 port (oracle/ddc_oracle.c, kind "port") on this host, 1 thread,
-    on a bounded sample of the same workload; also check the GPU output on that sample."""
-    sys.path.insert(0, ROOT)
-    from oracle import oracle as O
-    H32 = O.filter_bank(1.0, np.float32)
-    O.r2iq(sample_in, 1, d, tunebin, dtype=np.float32, H=H32)      # warm tables
-    done, t0 = 0, time.perf_counter()
-    while True:
-        O.r2iq(sample_in, nblk_sample, d, tunebin, dtype=np.float32, H=H32)
-        done += nblk_sample
-        if time.perf_counter() - t0 >= budget_s:
-            break
-    dt = time.perf_counter() - t0
-    ref = O.r2iq(sample_in, nblk_sample, d, tunebin)                # f64 checker
-    err = O.max_rel_err(gpu_sample_out, ref)
-    cpu = "unknown"
+def _cpu_model() -> str:
     try:
         for line in subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout.splitlines():
             if line.startswith("Model name"):
-                cpu = line.split(":", 1)[1].strip()
+                return line.split(":", 1)[1].strip()
     except Exception:
         pass
+    return "unknown"
+
+
+def cpu_backend_rate(d: int, tunebin: int, sample_in: np.ndarray, nblk_sample: int, budget_s: float):
+    """The library's CPU backend (a handle on DEVICE_CPU: the AVX2 restatement of the reference's
+    Core/fft_mt_r2iq_avx2.cpp worker, extio_sddc_amd/csrc/cpu/) on this thread, over a bounded
+    sample: (input MS/s, seconds timed, its output on the sample)."""
+    from extio_sddc_amd import DEVICE_CPU, R2iq, output_samples
+    blocks = np.ascontiguousarray(sample_in[HALF: HALF + nblk_sample * BLOCK])
+    out = np.empty((output_samples(d, nblk_sample), 2), np.float32)
+    with R2iq(gain=1.0, device=DEVICE_CPU) as r:
+        assert r.backend == "cpu"
+        r.setDecimate(d)
+        r.setTuneBin(tunebin)
+        L, h = r._L, r._h
+        L.sddc_ddc_process_host(h, blocks.ctypes.data, nblk_sample, out.ctypes.data)   # warm tables, pages
+        done, t0 = 0, time.perf_counter()
+        while True:
+            L.sddc_ddc_process_host(h, blocks.ctypes.data, nblk_sample, out.ctypes.data)
+            done += nblk_sample
+            if time.perf_counter() - t0 >= budget_s:
+                break
+        dt = time.perf_counter() - t0
+        r.TurnOn()   # zero history: the output of the sample from the stream start
+        y = r.process(blocks)
+    return done * BLOCK / dt / 1e6, dt, y
+
+
+def cpu_baseline(d: int, tunebin: int, gpu_sample_out, sample_in: np.ndarray, nblk_sample: int,
+                 budget_s: float, oracle_port_s: float = 3.0) -> dict:
+    """cpu_baseline (1 core): the library's AVX2 CPU backend, timed on this host's core over a
+    bounded sample of the same workload; the oracle's scalar float32 port (oracle/ddc_oracle.c)
+    is timed next to it for reference.  Also checks the GPU's and the CPU backend's output on
+    the sample against the f64 oracle."""
+    sys.path.insert(0, ROOT)
+    from oracle import oracle as O
+    v, dt, ycpu = cpu_backend_rate(d, tunebin, sample_in, nblk_sample, budget_s)
+    H32 = O.filter_bank(1.0, np.float32)
+    O.r2iq(sample_in, 1, d, tunebin, dtype=np.float32, H=H32)      # warm tables
+    done, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < oracle_port_s:
+        O.r2iq(sample_in, nblk_sample, d, tunebin, dtype=np.float32, H=H32)
+        done += nblk_sample
+    port = done * BLOCK / (time.perf_counter() - t0) / 1e6
+    ref = O.r2iq(sample_in, nblk_sample, d, tunebin)                # f64 checker
     return {
-        "value": done * BLOCK / dt / 1e6, "unit": "input MSamples/s", "cores": 1, "kind": "port",
-        "sample": f"{nblk_sample} blocks x 65536 int16 (tone mix), repeated for {dt:.1f} s, "
-                  f"d={d}, tunebin={tunebin}, float32 oracle port, 1 thread",
-        "cpu_model": cpu, "host_nproc": os.cpu_count(),
-        "iq_max_rel_err_gpu_vs_oracle_f64": err,
+        "value": v, "unit": "input MSamples/s", "cores": 1, "kind": "port",
+        "sample": f"{nblk_sample} blocks x 65536 int16 (tone mix), repeated for {dt:.1f} s, d={d}, "
+                  f"tunebin={tunebin}: the library's AVX2 CPU backend (restatement of "
+                  f"Core/fft_mt_r2iq_avx2.cpp without FFTW), 1 thread",
+        "cpu_model": _cpu_model(), "host_nproc": os.cpu_count(),
+        "oracle_f32_port_1core_MSps": port,
+        "iq_max_rel_err_cpu_backend_vs_oracle_f64": O.max_rel_err(ycpu, ref),
+        "iq_max_rel_err_gpu_vs_oracle_f64": O.max_rel_err(gpu_sample_out, ref),
         "iq_rms_rel_err_gpu_vs_oracle_f64": O.rms_rel_err(gpu_sample_out, ref),
     }
 
 
+# one CPU-backend instance, pinned to one CPU; ctypes only (no torch, never touches a GPU)
 _CPU_WORKER = r"""
-import sys, time, numpy as np
-sys.path.insert(0, sys.argv[1])
-from oracle import oracle as O
-x = np.load(sys.argv[2]); nblk, d, tb, budget = int(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5]), float(sys.argv[6])
-H = O.filter_bank(1.0, np.float32)
-O.r2iq(x, 1, d, tb, dtype=np.float32, H=H)
+import ctypes, os, sys, time, numpy as np
+lib_path, x_path, nblk, d, tb, budget, cpu = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5]), float(sys.argv[6]), int(sys.argv[7])
+os.sched_setaffinity(0, {cpu})
+L = ctypes.CDLL(lib_path)
+P = ctypes.c_void_p
+L.sddc_ddc_create.argtypes = [ctypes.c_float, ctypes.c_int, ctypes.POINTER(P)]
+for f in ("sddc_ddc_set_decimation", "sddc_ddc_set_tunebin"): getattr(L, f).argtypes = [P, ctypes.c_int]
+L.sddc_ddc_process_host.argtypes = [P, P, ctypes.c_int, P]
+h = P()
+assert L.sddc_ddc_create(1.0, -1, ctypes.byref(h)) == 0
+assert L.sddc_ddc_set_decimation(h, d) == 0 and L.sddc_ddc_set_tunebin(h, tb) == 0
+x = np.ascontiguousarray(np.load(x_path)[4096:4096 + nblk * 65536])
+out = np.empty(nblk * (32768 >> d) * 2, np.float32)
+L.sddc_ddc_process_host(h, x.ctypes.data, nblk, out.ctypes.data)
 done, t0 = 0, time.perf_counter()
 while time.perf_counter() - t0 < budget:
-    O.r2iq(x, nblk, d, tb, dtype=np.float32, H=H); done += nblk
+    assert L.sddc_ddc_process_host(h, x.ctypes.data, nblk, out.ctypes.data) == 0; done += nblk
 print(done, time.perf_counter() - t0)
 """
 
 
-def cpu_baseline_all_cores(d: int, tunebin: int, sample_in: np.ndarray, nblk_sample: int, budget_s: float) -> dict:
-    """one independent f32-port instance per core of this process's CPU
-    share (at most 16, the GPU box's share), as child processes that never touch the GPU."""
-    import tempfile
+def _distinct_core_cpus(limit: int):
+    """CPUs of this process's affinity set, at most one per physical core (SMT siblings
+    skipped), at most `limit` (the GPU box's CPU share is 16)."""
     try:
-        ncores = len(os.sched_getaffinity(0))
+        aff = sorted(os.sched_getaffinity(0))
     except AttributeError:
-        ncores = os.cpu_count() or 1
-    procs = max(1, min(16, ncores))
+        aff = list(range(os.cpu_count() or 1))
+    picked, seen = [], set()
+    for c in aff:
+        try:
+            with open(f"/sys/devices/system/cpu/cpu{c}/topology/core_id") as f:
+                core = f.read().strip()
+            with open(f"/sys/devices/system/cpu/cpu{c}/topology/physical_package_id") as f:
+                pkg = f.read().strip()
+            key = (pkg, core)
+        except OSError:
+            key = c
+        if key in seen:
+            continue
+        seen.add(key)
+        picked.append(c)
+        if len(picked) >= limit:
+            break
+    return picked, len(aff)
+
+
+def cpu_baseline_all_cores(d: int, tunebin: int, sample_in: np.ndarray, nblk_sample: int, budget_s: float) -> dict:
+    """one independent CPU-backend instance per physical core of this
+    process's CPU share (at most 16, the GPU box's share), each a child process pinned to its own
+    core that never touches the GPU; aggregate input MS/s."""
+    import tempfile
+    from extio_sddc_amd._lib import LIB_PATH
+    cpus, naff = _distinct_core_cpus(16)
     with tempfile.TemporaryDirectory(dir="/tmp") as td:
         path = os.path.join(td, "sample.npy")
         np.save(path, sample_in)
         env = dict(os.environ, OMP_NUM_THREADS="1")
-        ps = [subprocess.Popen([sys.executable, "-c", _CPU_WORKER, ROOT, path, str(nblk_sample), str(d), str(tunebin),
-                                str(budget_s)], stdout=subprocess.PIPE, text=True, env=env) for _ in range(procs)]
+        ps = [subprocess.Popen([sys.executable, "-c", _CPU_WORKER, LIB_PATH, path, str(nblk_sample), str(d),
+                                str(tunebin), str(budget_s), str(c)], stdout=subprocess.PIPE, text=True, env=env)
+              for c in cpus]
         total = 0.0
         for p in ps:
             out, _ = p.communicate(timeout=budget_s * 4 + 60)
             done, dt = out.split()
             total += int(done) * BLOCK / float(dt)
-    return {"value": total / 1e6, "unit": "input MSamples/s", "cores": procs, "kind": "port",
-            "sample": f"{procs} independent processes x the 1-core sample, {budget_s:.1f} s each"}
+    return {"value": total / 1e6, "unit": "input MSamples/s", "cores": len(cpus), "kind": "port",
+            "cpus": cpus, "affinity_cpus": naff,
+            "sample": f"{len(cpus)} independent CPU-backend processes, one per physical core (pinned), "
+                      f"x the 1-core sample, {budget_s:.1f} s each"}
 
 
-def reference_equivalent(port_msps: float, d: int):
-    """Scale an on-box port timing by the committed port-vs-reference ratio
+def reference_equivalent(backend_msps: float, d: int):
+    """Scale an on-box CPU-backend timing by the committed backend-vs-reference ratio
     (profiles/cpu_calibration.json, tools/cpu_calib.py): an estimate, labelled as such."""
     try:
         with open(os.path.join(ROOT, "profiles", "cpu_calibration.json")) as f:
-            r = json.load(f)["ratio_reference_over_port"][str(d)]
-        return {"value": port_msps * r, "ratio": r,
-                "basis": "reference AVX2 r2iq / f32 port, both 1 core of the survey container (BASELINE.md §2)"}
+            r = json.load(f)["ratio_reference_over_avx2_backend"][str(d)]
+        return {"value": backend_msps * r, "ratio": r,
+                "basis": "reference AVX2 r2iq (survey probe) / this library's AVX2 backend, both 1 core of the "
+                         "survey container type (tools/cpu_calib.py)"}
     except Exception:
         return None
 
@@ -407,6 +475,7 @@ def main() -> None:
             cb["all_cores"] = {"error": str(e)}
         cb["reference_equivalent_estimate"] = reference_equivalent(cb["value"], d)
         result["cpu_baseline"] = cb
+        result["gpu_over_cpu_backend_1core"] = value / cb["value"]
         result["iq_max_rel_err"] = cb.pop("iq_max_rel_err_gpu_vs_oracle_f64")
         result["iq_rms_rel_err"] = cb.pop("iq_rms_rel_err_gpu_vs_oracle_f64")
     if sweep:
@@ -417,8 +486,9 @@ def main() -> None:
                 ddc.process_device(d_in, ns, d_out, stream)
                 torch.cuda.synchronize()
                 gout = d_out[: output_samples(dd, ns) * 2].cpu().numpy().view(np.complex64)
-                cbd = cpu_baseline(dd, args.tunebin, gout, d_in[: HALF + ns * BLOCK].cpu().numpy(), ns, 2.0)
-                line["cpu_port_1core_MSps"] = cbd["value"]
+                cbd = cpu_baseline(dd, args.tunebin, gout, d_in[: HALF + ns * BLOCK].cpu().numpy(), ns, 2.0, 1.0)
+                line["cpu_backend_1core_MSps"] = cbd["value"]
+                line["cpu_oracle_port_1core_MSps"] = cbd["oracle_f32_port_1core_MSps"]
                 line["cpu_reference_equivalent_MSps"] = (reference_equivalent(cbd["value"], dd) or {}).get("value")
                 line["iq_max_rel_err"] = cbd["iq_max_rel_err_gpu_vs_oracle_f64"]
         result["sweep"] = sweep

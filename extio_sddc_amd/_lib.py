@@ -2,7 +2,9 @@
 
 The library is the in-tree ``extio_sddc_amd/lib/libsddc_ddc.so`` (built for
 gfx950 by ``make -C extio_sddc_amd/csrc``).  There is no fallback: if it is
-missing or cannot be loaded, every compute entry point raises.
+missing or cannot be loaded, every compute entry point raises.  Its CPU backend
+(device ``DEVICE_CPU``) lives in the same library and is only used when a handle
+is created on it explicitly.
 
 torch is imported (when installed) BEFORE the library is loaded: PyTorch-ROCm
 ships its own ``libamdhip64.so`` with the same soname (libamdhip64.so.7), and
@@ -33,6 +35,8 @@ SIGNATURES = {
     "sddc_ddc_filter_response": (_I, [_F, _I, _P]),
     "sddc_ddc_create": (_I, [_F, _I, ctypes.POINTER(_P)]),
     "sddc_ddc_destroy": (_I, [_P]),
+    "sddc_ddc_backend": (_I, [_P]),
+    "sddc_ddc_set_history": (_I, [_P, _P]),
     "sddc_ddc_set_decimation": (_I, [_P, _I]),
     "sddc_ddc_set_sideband": (_I, [_P, _I]),
     "sddc_ddc_set_rand": (_I, [_P, _I]),
@@ -54,6 +58,9 @@ SIGNATURES = {
     "sddc_fft_c2c": (_I, [_P, _P, _I, _I, _I, _P]),
     "sddc_fft_r2c": (_I, [_P, _P, _I, _I, _P]),
 }
+
+DEVICE_CPU = -1      # SDDC_DDC_DEVICE_CPU
+BACKEND_HIP, BACKEND_CPU = 0, 1
 
 ERRORS = {0: "SDDC_OK", -1: "SDDC_ERR_ARG", -2: "SDDC_ERR_HIP", -3: "SDDC_ERR_NODEV",
           -4: "SDDC_ERR_STATE", -5: "SDDC_ERR_NOMEM"}

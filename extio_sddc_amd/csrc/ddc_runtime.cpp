@@ -2,8 +2,9 @@
 //
 // Owns the per-handle device state that the reference keeps in fft_mt_r2iq
 // (Core/fft_mt_r2iq.h:86-117): the filter bank (filterHw), the FFT "plans"
-// (here: twiddle tables), the tune bin and the stream history.  There is no CPU
-// fallback: every compute call goes to the gfx950 kernels in ddc_kernels.hip.
+// (here: twiddle tables), the tune bin and the stream history.  A GPU handle's compute
+// calls go to the gfx950 kernels only (no fallback); a handle created on
+// SDDC_DDC_DEVICE_CPU holds the AVX2 backend (cpu/r2iq_cpu.h) instead and never calls HIP.
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
@@ -11,12 +12,15 @@
 #include <complex>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <new>
 #include <string>
 #include <vector>
 
+#include "cpu/r2iq_cpu.h"
 #include "ddc_kernels.h"
 #include "filterbank.h"
 #include "fine_tune.h"
@@ -179,7 +183,23 @@ struct sddc_ddc {
     int nco_slot = 0;
     float2 *d_nco = nullptr;
     size_t d_nco_cap = 0;
+
+    // history to start the next host-path call from (sddc_ddc_set_history)
+    std::vector<int16_t> hist_override;
+
+    // CPU handle (device SDDC_DDC_DEVICE_CPU): the AVX2 backend; no HIP object above exists
+    std::unique_ptr<sddc::cpu::R2iq> cpu;
+
+    // fault injection for failover tests (GPU handles): environment SDDC_DDC_INJECT_FAIL=N
+    // makes the (N+1)-th process_* call fail with SDDC_ERR_HIP before any device work
+    long inject_fail = -1;
 };
+
+static bool injected_failure(sddc_ddc_t *h)
+{
+    if (h->inject_fail < 0) return false;
+    return h->inject_fail-- == 0;
+}
 
 extern "C" {
 
@@ -228,6 +248,24 @@ int sddc_ddc_create(float gain, int device, sddc_ddc_t **out)
 {
     if (!out) return fail(SDDC_ERR_ARG, "create: null out");
     *out = nullptr;
+    if (device == SDDC_DDC_DEVICE_CPU) {
+        if (!sddc::cpu::supported()) return fail(SDDC_ERR_NODEV, "create: the CPU backend needs AVX2 and FMA");
+        auto *h = new (std::nothrow) sddc_ddc();
+        if (!h) return fail(SDDC_ERR_NOMEM, "create: out of host memory");
+        h->device = SDDC_DDC_DEVICE_CPU;
+        h->gain = gain;
+        try {
+            std::vector<std::complex<double>> H((size_t)SDDC_DDC_NDEC * SDDC_DDC_HALF_FFT);
+            for (int d = 0; d < SDDC_DDC_NDEC; d++) sddc::filter_response(gain, d, H.data() + (size_t)d * SDDC_DDC_HALF_FFT);
+            h->cpu.reset(new sddc::cpu::R2iq(H.data()));
+        } catch (const std::exception &ex) {
+            delete h;
+            return fail(SDDC_ERR_NOMEM, "create: %s", ex.what());
+        }
+        *out = h;
+        return SDDC_OK;
+    }
+    if (device < 0) return fail(SDDC_ERR_ARG, "create: device %d (>= 0, or SDDC_DDC_DEVICE_CPU)", device);
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
         return fail(SDDC_ERR_NODEV, "create: no HIP device visible");
@@ -245,6 +283,7 @@ int sddc_ddc_create(float gain, int device, sddc_ddc_t **out)
     if (!h) return fail(SDDC_ERR_NOMEM, "create: out of host memory");
     h->device = device;
     h->gain = gain;
+    if (const char *inj = std::getenv("SDDC_DDC_INJECT_FAIL")) h->inject_fail = std::atol(inj);
 
     // ---- constant tables (one device allocation) ----
     auto W = [](double num, double den) {   // e^{-2 pi i num/den}, double -> float once
@@ -324,9 +363,19 @@ int sddc_ddc_create(float gain, int device, sddc_ddc_t **out)
     return SDDC_OK;
 }
 
+int sddc_ddc_backend(const sddc_ddc_t *h)
+{
+    if (!h) return fail(SDDC_ERR_ARG, "null handle");
+    return h->cpu ? SDDC_DDC_BACKEND_CPU : SDDC_DDC_BACKEND_HIP;
+}
+
 int sddc_ddc_destroy(sddc_ddc_t *h)
 {
     if (!h) return SDDC_OK;
+    if (h->cpu) {
+        delete h;
+        return SDDC_OK;
+    }
     {
         DeviceGuard g(h->device);
         if (h->stream) (void)hipStreamSynchronize(h->stream);
@@ -425,6 +474,20 @@ int sddc_ddc_reset(sddc_ddc_t *h)
     if (!h) return fail(SDDC_ERR_ARG, "null handle");
     std::lock_guard<std::mutex> lk(h->mu);
     h->last_slot = -1;   // the next host-path chunk starts from a zero history
+    h->hist_override.clear();
+    if (h->cpu) h->cpu->reset();
+    return SDDC_OK;
+}
+
+int sddc_ddc_set_history(sddc_ddc_t *h, const int16_t *last4096)
+{
+    if (!h || !last4096) return fail(SDDC_ERR_ARG, "set_history: null handle or samples");
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (h->cpu) {
+        h->cpu->set_history(last4096);
+        return SDDC_OK;
+    }
+    h->hist_override.assign(last4096, last4096 + kHistory);
     return SDDC_OK;
 }
 
@@ -573,8 +636,10 @@ int sddc_ddc_process_device(sddc_ddc_t *h, const int16_t *d_in, int nblk, void *
 {
     if (!h) return fail(SDDC_ERR_ARG, "null handle");
     std::lock_guard<std::mutex> lk(h->mu);   // the call reads d, format, tune bin: one consistent set
+    if (h->cpu) return fail(SDDC_ERR_STATE, "process_device: a CPU handle has no device path");
     int rc = check_process_args(h, d_in, nblk, d_out);
     if (rc) return rc;
+    if (injected_failure(h)) return fail(SDDC_ERR_HIP, "injected failure (SDDC_DDC_INJECT_FAIL)");
     DeviceGuard g(h->device);
     HIP_TRY(g.err);
     HIP_TRY(launch_single(h, d_in, nblk, d_out, (hipStream_t)hip_stream));
@@ -586,6 +651,7 @@ int sddc_ddc_process_channels_device(sddc_ddc_t *h, const int16_t *d_in, int nbl
 {
     if (!h) return fail(SDDC_ERR_ARG, "null handle");
     std::lock_guard<std::mutex> lk(h->mu);   // d, format and NCO state are read below
+    if (h->cpu) return fail(SDDC_ERR_STATE, "process_channels_device: a CPU handle has no device path");
     int rc = check_process_args(h, d_in, nblk, d_out);
     if (rc) return rc;
     if (!tunebins || nch <= 0 || nch > SDDC_DDC_MAX_CHANNELS)
@@ -721,7 +787,12 @@ static int host_pipeline(sddc_ddc_t *h, int nblk, Src src, void *out)
         auto &sl = h->hs[slot];
         // ---- input: history, then the blocks ----
         HIP_TRY(hipStreamWaitEvent(s_in, sl.e_k, 0));
-        if (h->last_slot < 0) {
+        if (!h->hist_override.empty()) {   // sddc_ddc_set_history (pageable source: staged copy)
+            HIP_TRY(hipMemcpyAsync(sl.d_in, h->hist_override.data(), kHistory * sizeof(int16_t),
+                                   hipMemcpyHostToDevice, s_in));
+            HIP_TRY(hipStreamSynchronize(s_in));   // the vector is cleared below
+            h->hist_override.clear();
+        } else if (h->last_slot < 0) {
             HIP_TRY(hipMemsetAsync(sl.d_in, 0, kHistory * sizeof(int16_t), s_in));
         } else {
             const auto &prev = h->hs[h->last_slot];
@@ -774,12 +845,44 @@ static int host_pipeline(sddc_ddc_t *h, int nblk, Src src, void *out)
 }
 }  // extern "C++"
 
+// CPU handle: the whole call on the calling thread (cpu/r2iq_cpu.h)
+static int cpu_process(sddc_ddc_t *h, const int16_t *const *blocks, int nblk, void *out)
+{
+    sddc::cpu::Params p;
+    p.d = h->d;
+    p.tunebin = h->tunebin;
+    p.lsb = h->lsb != 0;
+    p.rand = h->rand != 0;
+    p.cs16 = h->out_fmt == SDDC_DDC_FMT_CS16;
+    p.scale = h->cs16_scale;
+    std::vector<float2> starts;
+    if (h->nco_fc != 0.f) {
+        const long nb = (long)nblk * (SDDC_DDC_OUT_BLOCK >> h->d) / sddc::FineTune::kBlock;
+        starts.resize((size_t)nb * sddc::FineTune::kLanes);
+        h->nco.starts(nb, starts.data());
+        p.nco_trig = reinterpret_cast<const float *>(h->nco.table());
+        p.nco_starts = reinterpret_cast<const float *>(starts.data());
+    }
+    try {
+        h->cpu->process(blocks, nblk, out, p);
+    } catch (const std::exception &ex) {
+        return fail(SDDC_ERR_NOMEM, "cpu backend: %s", ex.what());
+    }
+    return SDDC_OK;
+}
+
 int sddc_ddc_process_host(sddc_ddc_t *h, const int16_t *in, int nblk, void *out)
 {
     if (!h) return fail(SDDC_ERR_ARG, "null handle");
     std::lock_guard<std::mutex> lk(h->mu);
     int rc = check_process_args(h, in, nblk, out);
     if (rc) return rc;
+    if (h->cpu) {
+        std::vector<const int16_t *> blocks((size_t)nblk);
+        for (int i = 0; i < nblk; i++) blocks[i] = in + (size_t)i * kBlock;
+        return cpu_process(h, blocks.data(), nblk, out);
+    }
+    if (injected_failure(h)) return fail(SDDC_ERR_HIP, "injected failure (SDDC_DDC_INJECT_FAIL)");
     DeviceGuard g(h->device);
     HIP_TRY(g.err);
     return host_pipeline(h, nblk, [in](int i) { return in + (size_t)i * kBlock; }, out);
@@ -794,6 +897,8 @@ int sddc_ddc_process_blocks(sddc_ddc_t *h, const int16_t *const *blocks, int nbl
     if (rc) return rc;
     for (int i = 0; i < nblk; i++)
         if (!blocks[i] || ((uintptr_t)blocks[i] & 3)) return fail(SDDC_ERR_ARG, "block %d null or unaligned", i);
+    if (h->cpu) return cpu_process(h, blocks, nblk, out);
+    if (injected_failure(h)) return fail(SDDC_ERR_HIP, "injected failure (SDDC_DDC_INJECT_FAIL)");
     DeviceGuard g(h->device);
     HIP_TRY(g.err);
     return host_pipeline(h, nblk, [blocks](int i) { return blocks[i]; }, out);
@@ -802,13 +907,15 @@ int sddc_ddc_process_blocks(sddc_ddc_t *h, const int16_t *const *blocks, int nbl
 int sddc_ddc_register_host(sddc_ddc_t *h, void *ptr, size_t bytes)
 {
     if (!h || !ptr || !bytes) return fail(SDDC_ERR_ARG, "register_host: null handle/pointer or zero size");
-    DeviceGuard g(h->device);
-    HIP_TRY(g.err);
     std::lock_guard<std::mutex> lk(h->mu);
     for (const auto &r : h->regions)
         if (static_cast<char *>(ptr) < r.first + r.second && r.first < static_cast<char *>(ptr) + bytes)
             return fail(SDDC_ERR_ARG, "register_host: overlaps a registered region");
-    HIP_TRY(hipHostRegister(ptr, bytes, hipHostRegisterDefault));
+    if (!h->cpu) {   // a CPU handle reads host memory directly: bookkeeping only
+        DeviceGuard g(h->device);
+        HIP_TRY(g.err);
+        HIP_TRY(hipHostRegister(ptr, bytes, hipHostRegisterDefault));
+    }
     h->regions.emplace_back(static_cast<const char *>(ptr), bytes);
     return SDDC_OK;
 }
@@ -816,13 +923,15 @@ int sddc_ddc_register_host(sddc_ddc_t *h, void *ptr, size_t bytes)
 int sddc_ddc_unregister_host(sddc_ddc_t *h, void *ptr)
 {
     if (!h || !ptr) return fail(SDDC_ERR_ARG, "unregister_host: null handle/pointer");
-    DeviceGuard g(h->device);
-    HIP_TRY(g.err);
     std::lock_guard<std::mutex> lk(h->mu);
     for (size_t i = 0; i < h->regions.size(); i++) {
         if (h->regions[i].first == ptr) {
             // in-flight host-path copies finished when process_* returned (synchronous)
-            HIP_TRY(hipHostUnregister(ptr));
+            if (!h->cpu) {
+                DeviceGuard g(h->device);
+                HIP_TRY(g.err);
+                HIP_TRY(hipHostUnregister(ptr));
+            }
             h->regions.erase(h->regions.begin() + (long)i);
             return SDDC_OK;
         }

@@ -37,6 +37,13 @@ static_assert(LayoutProbe::dec() == 8 && LayoutProbe::on() == 12 && LayoutProbe:
 #pragma GCC diagnostic pop
 
 static constexpr int kBlock = 65536;     // transferSamples, config.h:80-81
+
+// r2iqOn is a plain bool of the ABI-fixed base class (Core/r2iq.h), written by TurnOn/TurnOff
+// on the caller's thread and polled by the worker and writer threads.  Every access here is an
+// atomic one on that same byte (acquire/release), so the layout stays and the accesses do not
+// race (the reference reads it unsynchronised, impl.hpp:15; found by the TSan build).
+bool fft_mt_r2iq::on() const { return __atomic_load_n(&r2iqOn, __ATOMIC_ACQUIRE); }
+void fft_mt_r2iq::set_on(bool v) { __atomic_store_n(&r2iqOn, v, __ATOMIC_RELEASE); }
 static constexpr int kMaxBatch = 16;     // input blocks per GPU call (<= half the 32-transfer queue)
 
 // The contiguous storage behind a ring's slots (ringbuffer::setBlockSize allocates all
@@ -78,6 +85,50 @@ fft_mt_r2iq::fft_mt_r2iq() : r2iqControlClass()
     device_ = dev ? std::atoi(dev) : 0;
 }
 
+const char *fft_mt_r2iq::backendName() const
+{
+    const int b = backend_.load();
+    return b == SDDC_DDC_BACKEND_CPU ? "cpu" : b == SDDC_DDC_BACKEND_HIP ? "hip" : "none";
+}
+
+// A fresh handle on `device` (or SDDC_DDC_DEVICE_CPU) with the output stages registered.
+bool fft_mt_r2iq::create_handle(int device)
+{
+    if (ddc_) {
+        sddc_ddc_destroy(ddc_);
+        ddc_ = nullptr;
+        backend_.store(-1);
+    }
+    if (sddc_ddc_create(GainScale, device, &ddc_) != SDDC_OK) {
+        ddc_ = nullptr;
+        return false;
+    }
+    backend_.store(sddc_ddc_backend(ddc_));
+    for (auto &st : out_stage_)   // pinned for direct D2H; on failure the library stages through its own buffers
+        (void)sddc_ddc_register_host(ddc_, st.data(), st.size() * sizeof(float));
+    return true;
+}
+
+// SDDC_DDC_BACKEND=auto after a GPU failure in the worker: continue on a CPU handle from the
+// same stream position.  The history is the tail of the last block taken (still readable at
+// peekReadPtr(-1), Core/dsp/ringbuffer.h; the reference reads it there, impl.hpp:32).
+bool fft_mt_r2iq::switch_to_cpu(uint64_t consumed)
+{
+    std::fprintf(stderr, "[fft_mt_r2iq] GPU backend failed (%s); SDDC_DDC_BACKEND=auto: continuing on the CPU\n",
+                 last_error_.c_str());
+    if (in_region_) {   // the GPU handle's registration goes with it
+        (void)sddc_ddc_unregister_host(ddc_, in_region_);
+        in_region_ = nullptr;
+    }
+    if (!create_handle(SDDC_DDC_DEVICE_CPU)) return false;
+    if (sddc_ddc_set_decimation(ddc_, mdecimation) || sddc_ddc_set_sideband(ddc_, getSideband()) ||
+        sddc_ddc_reset(ddc_))
+        return false;
+    if (consumed > 0 && sddc_ddc_set_history(ddc_, inputbuffer->peekReadPtr(-1) + kBlock - halfFft))
+        return false;
+    return true;
+}
+
 fft_mt_r2iq::~fft_mt_r2iq()
 {
     if (worker_.joinable()) TurnOff();
@@ -107,20 +158,19 @@ void fft_mt_r2iq::Init(float gain, ringbuffer<int16_t> *input, ringbuffer<float>
     inputbuffer = input;
     outputbuffer = obuffers;
     GainScale = gain;
-    if (ddc_) {
-        sddc_ddc_destroy(ddc_);
-        ddc_ = nullptr;
-    }
-    if (sddc_ddc_create(gain, device_, &ddc_) != SDDC_OK) {
-        ddc_ = nullptr;
-        fail("Init: sddc_ddc_create");
-        return;
-    }
-    for (auto &st : out_stage_) {
-        st.assign((size_t)kMaxBatch * 8 * halfFft * 2, 0.f);
-        // pinned for direct D2H; on failure the library stages through its own buffers
-        (void)sddc_ddc_register_host(ddc_, st.data(), st.size() * sizeof(float));
-    }
+    const char *be = std::getenv("SDDC_DDC_BACKEND");
+    mode_ = !be || !std::strcmp(be, "hip") ? Backend::hip
+          : !std::strcmp(be, "cpu")        ? Backend::cpu
+          : !std::strcmp(be, "auto")       ? Backend::autoselect
+                                           : Backend::hip;
+    if (be && mode_ == Backend::hip && std::strcmp(be, "hip"))
+        std::fprintf(stderr, "[fft_mt_r2iq] SDDC_DDC_BACKEND=%s unknown (hip|cpu|auto): using hip\n", be);
+    for (auto &st : out_stage_) st.assign((size_t)kMaxBatch * 8 * halfFft * 2, 0.f);
+    if (create_handle(mode_ == Backend::cpu ? SDDC_DDC_DEVICE_CPU : device_)) return;
+    fail("Init: sddc_ddc_create");
+    if (mode_ != Backend::autoselect) return;
+    std::fprintf(stderr, "[fft_mt_r2iq] SDDC_DDC_BACKEND=auto: no usable GPU, using the CPU backend\n");
+    if (!create_handle(SDDC_DDC_DEVICE_CPU)) fail("Init: CPU backend");
 }
 
 void fft_mt_r2iq::TurnOn()
@@ -130,7 +180,7 @@ void fft_mt_r2iq::TurnOn()
         std::fprintf(stderr, "[fft_mt_r2iq] %s\n", last_error_.c_str());
         return;
     }
-    r2iqOn = true;
+    set_on(true);
     inputbuffer->Start();
     outputbuffer->Start();
     void *base = nullptr;
@@ -146,7 +196,7 @@ void fft_mt_r2iq::TurnOn()
 
 void fft_mt_r2iq::TurnOff(void)
 {
-    r2iqOn = false;
+    set_on(false);
     if (inputbuffer) inputbuffer->Stop();
     if (outputbuffer) outputbuffer->Stop();
     {
@@ -161,7 +211,7 @@ void fft_mt_r2iq::TurnOff(void)
     }
 }
 
-bool fft_mt_r2iq::IsOn(void) { return r2iqOn; }
+bool fft_mt_r2iq::IsOn(void) { return on(); }
 
 // Worker: input ring -> GPU -> out_stage_[k % 2].  Writer: out_stage_ -> output ring, so
 // the ring copy of batch k overlaps the GPU round trip of batch k + 1.
@@ -172,21 +222,21 @@ void fft_mt_r2iq::worker()
     const bool lsb = getSideband();
     if (sddc_ddc_set_decimation(ddc_, d) || sddc_ddc_set_sideband(ddc_, lsb) || sddc_ddc_reset(ddc_)) {
         fail("worker: configure");
-        r2iqOn = false;
+        set_on(false);
         std::lock_guard<std::mutex> lk(stage_mu_);
         stage_cv_.notify_all();
         return;
     }
     int stage = 0;
-    while (r2iqOn) {
+    while (on()) {
         {
             std::unique_lock<std::mutex> lk(stage_mu_);
-            stage_cv_.wait(lk, [&] { return stage_n_[stage] == 0 || !r2iqOn; });
+            stage_cv_.wait(lk, [&] { return stage_n_[stage] == 0 || !on(); });
         }
-        if (!r2iqOn) break;
+        if (!on()) break;
         const int16_t *blocks[kMaxBatch];
         blocks[0] = inputbuffer->getReadPtr();           // blocks while empty
-        if (!r2iqOn) break;
+        if (!on()) break;
         // Tune bin and rand of each block are read as the worker takes that block, as the
         // reference reads them once per block (impl.hpp:20, 40).  One GPU call runs one
         // (tunebin, rand) pair, so a block whose values differ from the batch head's starts
@@ -201,13 +251,19 @@ void fft_mt_r2iq::worker()
             blocks[n] = inputbuffer->peekReadPtr(n);
             n++;
         }
-        if (sddc_ddc_set_tunebin(ddc_, tb) || sddc_ddc_set_rand(ddc_, rnd) ||
-            sddc_ddc_process_blocks(ddc_, blocks, n, out_stage_[stage].data())) {
+        int rc = sddc_ddc_set_tunebin(ddc_, tb) || sddc_ddc_set_rand(ddc_, rnd) ||
+                 sddc_ddc_process_blocks(ddc_, blocks, n, out_stage_[stage].data());
+        if (rc && mode_ == Backend::autoselect && backend_.load() == SDDC_DDC_BACKEND_HIP) {
             fail("worker: process");
-            r2iqOn = false;
+            rc = !switch_to_cpu(consumed_) || sddc_ddc_set_tunebin(ddc_, tb) || sddc_ddc_set_rand(ddc_, rnd) ||
+                 sddc_ddc_process_blocks(ddc_, blocks, n, out_stage_[stage].data());
+        }
+        if (rc) {
+            fail("worker: process");
+            set_on(false);
             break;
         }
-        if (!r2iqOn) break;                              // TurnOff reset the ring meanwhile
+        if (!on()) break;                              // TurnOff reset the ring meanwhile
         for (int i = 0; i < n; i++) inputbuffer->ReadDone();
         consumed_ += (uint64_t)n;
         {
@@ -233,7 +289,7 @@ void fft_mt_r2iq::writer()
         int n;
         {
             std::unique_lock<std::mutex> lk(stage_mu_);
-            stage_cv_.wait(lk, [&] { return stage_n_[stage] > 0 || !r2iqOn; });
+            stage_cv_.wait(lk, [&] { return stage_n_[stage] > 0 || !on(); });
             n = stage_n_[stage];
         }
         if (n == 0) break;                               // stopped with nothing pending
@@ -241,7 +297,7 @@ void fft_mt_r2iq::writer()
         for (int i = 0; i < n; i++) {
             const uint64_t slot = seq & mask;
             if (slot == 0) pout = outputbuffer->getWritePtr();   // impl.hpp:111-114
-            if (!r2iqOn) return;
+            if (!on()) return;
             std::memcpy(pout + slot * per_blk, src + (size_t)i * per_blk, per_blk * sizeof(float));
             if (slot == mask) outputbuffer->WriteDone();          // impl.hpp:141-145
             seq++;

@@ -67,7 +67,8 @@ def device_count() -> int:
 
 
 class R2iq:
-    """The DDC for one stream on one GPU (one handle = one r2iq worker)."""
+    """The DDC for one stream on one GPU (one handle = one r2iq worker).
+    ``device=DEVICE_CPU`` (-1) selects the library's AVX2 CPU backend instead (host path only)."""
 
     def __init__(self, gain: float = 1.0, device: int = 0):
         self._L = _lib.load()
@@ -82,6 +83,14 @@ class R2iq:
         self._fmt = FMT_CF32
 
     # -- lifecycle --------------------------------------------------------
+    @property
+    def backend(self) -> str:
+        """"hip" or "cpu": which backend this handle runs (sddc_ddc_backend)."""
+        rc = self._L.sddc_ddc_backend(self._h)
+        if rc < 0:
+            check(rc)
+        return "cpu" if rc == _lib.BACKEND_CPU else "hip"
+
     def close(self) -> None:
         if getattr(self, "_h", None) is not None and self._h.value:
             self._L.sddc_ddc_destroy(self._h)
@@ -141,6 +150,13 @@ class R2iq:
 
     def TurnOn(self) -> None:
         check(self._L.sddc_ddc_reset(self._h))
+
+    def setHistory(self, last4096: np.ndarray) -> None:
+        """The next host-path call starts from these 4096 samples as its history."""
+        h = np.ascontiguousarray(last4096, np.int16).reshape(-1)
+        if h.size != HALF_FFT:
+            raise DDCError(-1, f"history must hold {HALF_FFT} samples")
+        check(self._L.sddc_ddc_set_history(self._h, h.ctypes.data))
 
     # -- the hot loop -----------------------------------------------------
     def setOutputFormat(self, fmt: str = "CF32", scale: float = 1.0) -> None:

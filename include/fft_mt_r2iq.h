@@ -18,8 +18,17 @@
  *     (impl.hpp:100-148);
  *   - TurnOff() stops both rings and joins the worker (fft_mt_r2iq.cpp:131-143).
  * Different by design: the worker may hand several already-queued input blocks to
- * the GPU in one launch (never waiting for more than the first); a GPU failure is
- * reported on stderr and through lastError() and the worker stops (no CPU fallback).
+ * the GPU in one launch (never waiting for more than the first).
+ *
+ * Backend (environment SDDC_DDC_BACKEND, read by Init):
+ *   hip  (default) the MI355X; no gfx950 device or a HIP error is reported on stderr and
+ *        through lastError(), and the worker stops — never a silent CPU run;
+ *   cpu  the library's AVX2 r2iq on the worker thread (the reference's
+ *        fft_mt_r2iq_avx2.cpp worker, restated without FFTW);
+ *   auto the MI355X, switching to the CPU backend — announced on stderr — when Init finds
+ *        no usable device or a GPU call fails mid-stream (the failed batch is redone on the
+ *        CPU from the same ring slots and history, so the output stream stays continuous).
+ * SDDC_DDC_DEVICE selects the GPU (default 0).
  */
 #pragma once
 
@@ -54,10 +63,16 @@ public:
     /* additions (not part of r2iqControlClass) */
     const char *lastError() const { return last_error_.c_str(); }
     uint64_t blocksProcessed() const { return blocks_done_.load(); }
+    /* "hip", "cpu" or "none" (no handle): the backend the worker runs on */
+    const char *backendName() const;
 
 private:
     void worker();
     void fail(const char *what);
+    bool create_handle(int device);
+    bool on() const;                  /* r2iqOn, read/written atomically */
+    void set_on(bool v);
+    bool switch_to_cpu(uint64_t consumed);
 
     ringbuffer<int16_t> *inputbuffer = nullptr;
     ringbuffer<float> *outputbuffer = nullptr;
@@ -65,8 +80,10 @@ private:
     int mfftdim[NDECIDX];
     std::atomic<int> mtunebin;
 
-    sddc_ddc *ddc_ = nullptr;         /* GPU handle (C ABI) */
+    sddc_ddc *ddc_ = nullptr;         /* DDC handle (C ABI) */
     int device_ = 0;
+    enum class Backend { hip, cpu, autoselect } mode_ = Backend::hip;
+    std::atomic<int> backend_{-1};    /* SDDC_DDC_BACKEND_* of ddc_, -1 = none */
     std::thread worker_;
     void writer();
 

@@ -8,6 +8,7 @@
  */
 #pragma once
 
+#include <atomic>
 #include <condition_variable>
 #include <cstdint>
 #include <mutex>
@@ -66,10 +67,11 @@ protected:
     }
 
     int slots;
-    volatile int rd = 0, wr = 0;
+    // read without the lock by peekReadPtr/peekWritePtr and the counters' getters: atomics
+    std::atomic<int> rd{0}, wr{0};
 
 private:
-    int empty_waits = 0, full_waits = 0, writes = 0;
+    std::atomic<int> empty_waits{0}, full_waits{0}, writes{0};
     bool stopped = false;
     std::mutex mu;
     std::condition_variable cv;

@@ -21,8 +21,15 @@
  * Errors: every int-returning call returns SDDC_OK (0) or a negative SDDC_ERR_*;
  * sddc_ddc_last_error() gives a thread-local message.  Nothing throws across this
  * boundary (the reference's r2iq methods are void/bool/float).
- * There is no CPU fallback: without a usable gfx950 device sddc_ddc_create()
- * fails with SDDC_ERR_NODEV.
+ *
+ * Backends.  A handle created on a device index >= 0 runs the gfx950 kernels; without a
+ * usable gfx950 device sddc_ddc_create() fails with SDDC_ERR_NODEV, and a HIP error fails
+ * the call — a GPU handle never falls back to the CPU.  A handle created on
+ * SDDC_DDC_DEVICE_CPU runs the library's AVX2 r2iq (the reference's fft_mt_r2iq_avx2.cpp
+ * worker, restated without FFTW) on the calling thread: the host path (process_host /
+ * process_blocks) with the same controls, output formats, fine-tune NCO and history
+ * semantics; its device-path calls return SDDC_ERR_STATE.  Choosing it is the caller's
+ * explicit decision (the drop-in class: SDDC_DDC_BACKEND=cpu|auto).
  */
 #ifndef SDDC_DDC_H
 #define SDDC_DDC_H
@@ -34,7 +41,8 @@
 extern "C" {
 #endif
 
-#define SDDC_DDC_ABI_VERSION 2   /* 2: + set_fine_tune, set_output_format, process_blocks, register_host */
+#define SDDC_DDC_ABI_VERSION 3   /* 2: + set_fine_tune, set_output_format, process_blocks, register_host;
+                                    3: + CPU handles (SDDC_DDC_DEVICE_CPU), backend, set_history */
 
 #define SDDC_DDC_HALF_FFT   4096    /* halfFft               fft_mt_r2iq.h:18 */
 #define SDDC_DDC_FFTN       8192    /* FFTN_R_ADC            config.h:49 */
@@ -58,6 +66,10 @@ enum {
 
 typedef struct sddc_ddc sddc_ddc_t;
 
+#define SDDC_DDC_DEVICE_CPU   (-1)  /* sddc_ddc_create(): the host AVX2 backend */
+#define SDDC_DDC_BACKEND_HIP  0
+#define SDDC_DDC_BACKEND_CPU  1
+
 /* ---- library ------------------------------------------------------------ */
 int         sddc_ddc_abi_version(void);
 const char *sddc_ddc_last_error(void);
@@ -80,6 +92,8 @@ int sddc_ddc_filter_response(float gain, int d, float *H /* [4096][2] */);
  * and uploads them with the FFT twiddle tables to `device`. */
 int sddc_ddc_create(float gain, int device, sddc_ddc_t **out);
 int sddc_ddc_destroy(sddc_ddc_t *h);
+/* SDDC_DDC_BACKEND_HIP or SDDC_DDC_BACKEND_CPU (negative on a null handle). */
+int sddc_ddc_backend(const sddc_ddc_t *h);
 
 /* ---- control: r2iqControlClass (r2iq.h:23-31) and fft_mt_r2iq -------------- */
 int   sddc_ddc_set_decimation(sddc_ddc_t *h, int d);        /* setDecimate   r2iq.h:31 */
@@ -95,6 +109,10 @@ float sddc_ddc_set_freq_offset(sddc_ddc_t *h, float offset);
 /* TurnOn() stream reset (fft_mt_r2iq.cpp:111-129): zero history, seq = 0.  The
  * fine-tune NCO keeps its phase (the reference's mixer state lives in RadioHandler). */
 int   sddc_ddc_reset(sddc_ddc_t *h);
+/* Host path: the next process_host/process_blocks call starts from these 4096 samples as
+ * its history instead of the kept one (the reference's peekReadPtr(-1) tail,
+ * fft_mt_r2iq_impl.hpp:32) — e.g. to continue a stream on another handle. */
+int   sddc_ddc_set_history(sddc_ddc_t *h, const int16_t *last4096);
 
 /* Fused fine-tune NCO: mixes the output with the reference's
  * fine-tune mixer, pf_mixer's shift_limited_unroll_C_sse (Core/pffft/pf_mixer.cpp:

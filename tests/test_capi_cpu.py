@@ -1,6 +1,7 @@
 """The C-ABI library on the CPU: it loads, exports every symbol include/sddc_ddc.h declares,
 its host-side filter design is bit-exact with the reference, and compute entry points
-fail loudly (SDDC_ERR_NODEV) when no GPU is present — there is no CPU fallback."""
+fail loudly (SDDC_ERR_NODEV) when no GPU is present — a GPU handle never falls back to
+the CPU (CPU handles are an explicit choice, tests/test_cpu_backend.py)."""
 from __future__ import annotations
 
 import ctypes
@@ -69,7 +70,7 @@ def test_filter_response_matches_oracle(ddc_lib, oracle):
 
 def test_output_samples_and_constants(ddc_lib):
     from extio_sddc_amd import output_samples
-    assert ddc_lib.sddc_ddc_abi_version() == 2
+    assert ddc_lib.sddc_ddc_abi_version() == 3
     for d in range(7):
         assert ddc_lib.sddc_ddc_output_samples(d, 3) == 3 * (32768 >> d) == output_samples(d, 3)
     assert ddc_lib.sddc_ddc_output_samples(7, 1) == 0

@@ -1,0 +1,54 @@
+"""Host sanitizers over the drop-in's threads (the reference's USE_DEBUG_ASAN,
+CMakeLists.txt:26-28): build/asan/r2iq_harness (-fsanitize=address,undefined) and
+build/tsan/r2iq_harness (-fsanitize=thread), built by `make -C extio_sddc_amd/csrc sanitize`,
+drive fft_mt_r2iq through r2iqControlClass on the CPU backend (SDDC_DDC_BACKEND=cpu): the
+worker and writer threads, both rings, the batch hand-off, per-block tune/rand changes and
+Start/Stop cycles, the C ABI front and the AVX2 r2iq.  Every run must be report-free and its
+IQ equal to the oracle's."""
+from __future__ import annotations
+
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from extio_sddc_amd.synth import make_stream
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPORTS = ("ERROR: AddressSanitizer", "ERROR: LeakSanitizer", "WARNING: ThreadSanitizer", "runtime error:")
+
+
+@pytest.fixture(scope="module")
+def harnesses():
+    p = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "extio_sddc_amd", "csrc"), "sanitize"],
+                       capture_output=True, text=True, timeout=900)
+    assert p.returncode == 0, p.stderr[-3000:]
+    return {k: os.path.join(ROOT, "build", k, "r2iq_harness") for k in ("asan", "tsan")}
+
+
+@pytest.mark.parametrize("kind", ["asan", "tsan"])
+@pytest.mark.parametrize("d,nblk,cycles,sched", [(1, 24, 3, "3:2048:1,7:284:0"), (4, 48, 2, "17:0:1")])
+def test_dropin_threads_under_sanitizer(tmp_path, oracle, harnesses, kind, d, nblk, cycles, sched):
+    x = make_stream(nblk, "mix")
+    fin, fout = tmp_path / "in.bin", tmp_path / "out.bin"
+    x[4096:].tofile(fin)
+    env = dict(os.environ, SDDC_DDC_BACKEND="cpu", R2IQ_SCHEDULE=sched,
+               ASAN_OPTIONS="detect_leaks=1:abort_on_error=0", TSAN_OPTIONS="halt_on_error=0")
+    p = subprocess.run([harnesses[kind], str(fin), str(nblk), str(d), "1024", "0", "0", "1.0", str(fout),
+                        str(cycles)], capture_output=True, text=True, timeout=600, env=env)
+    assert p.returncode == 0, p.stdout + p.stderr[-4000:]
+    for r in REPORTS:
+        assert r not in p.stderr, p.stderr[-4000:]
+    assert p.stdout.count(f"output blocks {nblk >> d} of {nblk >> d}") == cycles
+    y = np.fromfile(fout, np.float32).view(np.complex64).reshape(cycles, -1)
+    # first cycle: the schedule's (tune, rand) per block; later cycles: the last setting throughout
+    per = 32768 >> d
+    changes = [(0, 1024, 0)] + [tuple(int(v) for v in c.split(":")) for c in sched.split(",")] + [(nblk, 0, 0)]
+    for (a, tb, r), (b, _, _) in zip(changes[:-1], changes[1:]):
+        ref = oracle.r2iq(x[a * 65536: 4096 + b * 65536], b - a, d, tb, False, r)
+        assert oracle.max_rel_err(y[0, a * per: b * per], ref) <= 1e-5
+    last = changes[-2]
+    ref = oracle.r2iq(x, nblk, d, last[1], False, last[2])
+    for c in range(1, cycles):
+        assert oracle.max_rel_err(y[c], ref) <= 1e-5
