@@ -41,17 +41,23 @@ def algorithmic_bytes_per_sample(d: int, nch: int = 1, out_bytes: int = 8) -> fl
     return 2.0 + nch * float(out_bytes) / (1 << (d + 1))
 
 
-def make_input(torch, nblk: int, seed: int, device) -> "torch.Tensor":
-    """Synthetic 128 MS/s-labelled tone mix + noise (SURVEY.md §8(d) source (i)), int16 in HBM."""
-    n = nblk * BLOCK
-    g = torch.Generator(device=device).manual_seed(seed)
-    t = torch.arange(n, dtype=torch.float64, device=device)
+def make_input(torch, nblk: int, seed: int, device, first_block: int = 0) -> "torch.Tensor":
+    """Synthetic 128 MS/s-labelled tone mix + noise (SURVEY.md §8(d) source (i)), int16 in HBM:
+    blocks [first_block, first_block + nblk) of ONE global stream, preceded by its real 4096-sample
+    history (zeros at the stream start).  The noise is a counter-based function of the global
+    sample index, so rank r's segment and its halo are exactly the samples of the one stream that
+    rank r - 1's segment ends with (the time-segment hand-off of SURVEY.md §8(e))."""
+    s0 = first_block * BLOCK - HALF                      # global index of the buffer's first sample
+    t = torch.arange(s0, s0 + HALF + nblk * BLOCK, dtype=torch.float64, device=device)
     x = 9000 * torch.sin(2 * np.pi * 0.0713 * t) + 3000 * torch.sin(2 * np.pi * 0.191 * t)
-    del t
-    x += 300 * torch.randn(n, dtype=torch.float64, device=device, generator=g)
-    out = torch.zeros(HALF + n, dtype=torch.int16, device=device)
-    out[HALF:] = x.round().clamp_(-32768, 32767).to(torch.int16)
-    del x
+    # two uniforms per sample from a hash of (index, seed), then Box-Muller: N(0, 300)
+    u1 = torch.frac(torch.sin(t * 12.9898 + seed * 78.233) * 43758.5453).abs().clamp_(1e-12, 1.0)
+    u2 = torch.frac(torch.sin(t * 39.3468 + seed * 11.135) * 24634.6345).abs()
+    x += 300 * torch.sqrt(-2 * torch.log(u1)) * torch.cos(2 * np.pi * u2)
+    del u1, u2
+    out = x.round().clamp_(-32768, 32767).to(torch.int16)
+    out[t < 0] = 0                                        # before the stream start: zero history
+    del x, t
     return out
 
 
@@ -268,6 +274,9 @@ def main() -> None:
     ap.add_argument("--nblk", type=int, default=2048, help="blocks of 65536 per step per GPU")
     ap.add_argument("--mode", choices=["single", "channels"], default="single")
     ap.add_argument("--channels", type=int, default=1024)
+    ap.add_argument("--bcast", choices=["sag", "bcast"], default="sag",
+                    help="C5 input broadcast for N > 1: scatter + all-gather over all links (sag) or one "
+                         "broadcast collective (shard.broadcast_samples)")
     ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds of CPU-baseline work")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sweep", action="store_true",
@@ -319,8 +328,8 @@ def main() -> None:
     stream = torch.cuda.current_stream()
 
     if args.mode == "single":
-        # weak scaling: rank r owns stream segment r (its own blocks + halo)
-        d_in = make_input(torch, nblk, 0x5DDC + rank, dev)
+        # weak scaling: rank r owns segment r of one stream (its own blocks + the real halo)
+        d_in = make_input(torch, nblk, 0x5DDC, dev, first_block=rank * nblk)
         d_out = torch.empty(output_samples(d, nblk) * 2, dtype=out_dtype, device=dev)
         nch_local = 1
 
@@ -345,7 +354,7 @@ def main() -> None:
             # i + 1's broadcast runs while batch i is processed (double-buffered input)
             from extio_sddc_amd.shard import pipelined_batches
             d_in2 = d_in.clone()
-            batches = pipelined_batches([d_in, d_in2], None, src=0)   # unbounded; closed after timing
+            batches = pipelined_batches([d_in, d_in2], None, src=0, method=args.bcast)   # unbounded; closed after timing
 
             def step():
                 ddc.process_channels_device(next(batches), nblk, tbs, d_out, stream)
@@ -398,6 +407,34 @@ def main() -> None:
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall, kern_ms = t.tolist()
+
+    # N > 1 channels: the collective and the compute, each timed alone (max over ranks), so the
+    # line shows which of the two bounds the pipelined step
+    bcast_info = None
+    if args.mode == "channels" and world > 1:
+        from extio_sddc_amd.shard import broadcast_samples
+        reps = 10
+        res = []
+        for phase in ("broadcast", "compute"):
+            dist.barrier()
+            torch.cuda.synchronize()
+            tb0 = time.perf_counter()
+            for _ in range(reps):
+                if phase == "broadcast":
+                    broadcast_samples(d_in, src=0, method=args.bcast)
+                else:
+                    ddc.process_channels_device(d_in, nblk, tbs, d_out, stream)
+            torch.cuda.synchronize()
+            res.append((time.perf_counter() - tb0) / reps)
+        tt = torch.tensor(res, dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        b_s, c_s = tt.tolist()
+        batch_bytes = d_in.numel() * 2
+        bcast_info = {"method": args.bcast, "bytes_per_batch": batch_bytes, "ms": b_s * 1e3,
+                      "GBps_inbound_per_rank": batch_bytes / b_s / 1e9,
+                      "compute_ms_per_rank": c_s * 1e3, "reps": reps,
+                      "note": "each timed alone between barriers, max over ranks; the timed steps overlap "
+                              "batch i + 1's broadcast with batch i's compute"}
 
     # BASELINE.md §3 / SURVEY §8(d) C3 + C4 in the same run, while the clocks are at their
     # steady state: GPU rate and roofline per config (the headline value stays the d=0 line)
@@ -458,6 +495,8 @@ def main() -> None:
                      "compute": compute_roofline(workload, kern_ms)},
     }
 
+    if bcast_info:
+        result["broadcast"] = bcast_info
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         ns = 16
         sample = d_in[: HALF + ns * BLOCK].cpu().numpy()

@@ -5,6 +5,15 @@
   so segments are independent and outputs concatenate in order.
 - Channels (C5): contiguous tune-bin ranges per rank; every rank needs the whole
   int16 batch (broadcast from the ingest rank) and computes its own channels.
+
+The C5 input broadcast: one 128-channel shard of d = 4 runs at ~111 GS/s per
+GPU, i.e. ~222 GB/s of int16 into every GPU, more than one xGMI link (~153 GB/s) carries.  So
+the default broadcast is a scatter + all-gather ("sag"): the ingest rank sends 1/N of the
+batch to each rank (N - 1 point-to-point transfers leave it on N - 1 different links at once),
+then every rank all-gathers the N pieces, a collective that RCCL runs over all the links of
+the fully connected node.  The ingest rank's outbound bytes stay ~(N-1)/N of the batch (as
+for a plain broadcast) and every rank receives exactly one batch; no single link carries a
+whole batch.  "bcast" keeps the one-collective form for comparison.
 """
 from __future__ import annotations
 
@@ -30,16 +39,46 @@ def channel_shard(nch: int, world: int, rank: int) -> tuple[int, int]:
     return block_shard(nch, world, rank)
 
 
-def broadcast_samples(buf, src: int = 0) -> None:
-    """Broadcast an int16 sample batch from `src` to every rank.  NCCL/RCCL and gloo have
-    no int16 type, so the (even-length) batch travels as its int32 view — same bytes."""
+BROADCAST_METHODS = ("sag", "bcast")
+
+
+def broadcast_samples(buf, src: int = 0, method: str = "sag", async_op: bool = False):
+    """Send an int16 sample batch from `src` to every rank, in place.  NCCL/RCCL and gloo have
+    no int16 type, so the (even-length) batch travels as its int32 view — same bytes.
+
+    method "sag": scatter the batch in N equal pieces (piece r to rank r, in place), then
+    all-gather the pieces (in place); a remainder of fewer than N words is broadcast.
+    method "bcast": one broadcast collective.
+    async_op: return a work handle whose wait() orders the current stream (GPU) or blocks (CPU)
+    after the LAST collective of the method; collectives issued by one rank run in issue order."""
     import torch
     import torch.distributed as dist
     assert buf.dtype == torch.int16 and buf.numel() % 2 == 0 and buf.is_contiguous()
-    dist.broadcast(buf.view(torch.int32), src=src)
+    if method not in BROADCAST_METHODS:
+        raise ValueError(f"broadcast method {method!r} not in {BROADCAST_METHODS}")
+    w32 = buf.view(torch.int32)
+    world, rank = dist.get_world_size(), dist.get_rank()
+    if method == "bcast" or world == 1:
+        return dist.broadcast(w32, src=src, async_op=async_op)
+    piece = w32.numel() // world
+    last = None
+    if piece:
+        pieces = list(w32[: piece * world].view(world, piece).unbind(0))
+        mine = pieces[rank]
+        # RCCL runs one rank's collectives in issue order on its stream; gloo may run queued
+        # async collectives concurrently, so there the scatter completes first
+        sw = dist.scatter(mine, scatter_list=pieces if rank == src else None, src=src, async_op=async_op)
+        if async_op and dist.get_backend() == "gloo":
+            sw.wait()
+        last = dist.all_gather_into_tensor(w32[: piece * world], mine, async_op=async_op)
+    if piece * world < w32.numel():
+        if last is not None and async_op and dist.get_backend() == "gloo":
+            last.wait()
+        last = dist.broadcast(w32[piece * world:], src=src, async_op=async_op)
+    return last
 
 
-def pipelined_batches(bufs, nbatches: int, src: int = 0, fill=None):
+def pipelined_batches(bufs, nbatches: int, src: int = 0, fill=None, method: str = "sag"):
     """Yield nbatches input batches, bufs[i % 2] for batch i, every rank receiving the src
     rank's batch by broadcast, with the broadcast of batch i + 1 already in flight while the
     caller processes batch i (overlap the xGMI broadcast with the compute).
@@ -61,7 +100,7 @@ def pipelined_batches(bufs, nbatches: int, src: int = 0, fill=None):
         b = bufs[i % 2]
         if fill is not None and rank == src:
             fill(b, i)
-        return dist.broadcast(b.view(torch.int32), src=src, async_op=True)
+        return broadcast_samples(b, src=src, method=method, async_op=True)
 
     if nbatches is not None and nbatches <= 0:
         return

@@ -1,4 +1,4 @@
-"""N>1 data paths on CPU with gloo, world_size 2.
+"""N>1 data paths on CPU with gloo, world_size 2-4.
 
 - time segments (weak/strong scaling of one stream): each rank processes its own block
   range plus the 4096-sample halo; gathered outputs concatenate to the whole-stream result
@@ -8,6 +8,9 @@
   shards equal every channel computed on one rank.
 - pipelined broadcast (bench.py's C5 loop): with batch i + 1's broadcast in flight while batch
   i is used, every rank still sees every batch, in order, with the src rank's content.
+- broadcast methods (shard.broadcast_samples): scatter + all-gather ("sag", the default) and
+  one broadcast, at world 2, 3 and 4, blocking and async, even and uneven splits: every rank
+  ends with the src rank's bytes.
 The per-rank compute here is the oracle (no GPU); the partitioning, halo and collective
 logic is extio_sddc_amd.shard, the same code bench.py uses on the GPUs.
 """
@@ -55,6 +58,32 @@ def _worker(rank, world, port, mode, q):
                 full = O.r2iq(x, nblk, d, tb)
                 cat = np.concatenate([p[2] for p in sorted(parts, key=lambda p: p[0])])
                 q.put(bool(np.array_equal(cat, full)) and sum(p[1] - p[0] for p in parts) == nblk)
+        elif mode.startswith("bcast-"):
+            # every broadcast method: byte-identical batches on every rank, in order, incl. sizes
+            # that do not split evenly over the ranks (the remainder travels by broadcast)
+            from extio_sddc_amd.shard import broadcast_samples, pipelined_batches
+            method = mode.split("-", 1)[1]
+            ok = True
+            for n16 in (2 * 65536 + 4096, 2 * 7 * world + 2, 2):
+                ref = torch.from_numpy(make_stream(4, "uniform")[:n16].copy())
+                b = ref.clone() if rank == 0 else torch.zeros(n16, dtype=torch.int16)
+                broadcast_samples(b, src=0, method=method)
+                ok &= bool(torch.equal(b, ref))
+                b2 = ref.clone() if rank == 0 else torch.full((n16,), 7, dtype=torch.int16)
+                broadcast_samples(b2, src=0, method=method, async_op=True).wait()
+                ok &= bool(torch.equal(b2, ref))
+            stream = make_stream(8, "uniform")
+            bufs = [torch.zeros(4096 + 65536, dtype=torch.int16) for _ in range(2)]
+
+            def fill(b, i):
+                b.copy_(torch.from_numpy(stream[i * 65536:i * 65536 + b.numel()]))
+            seen = [b.numpy().copy() for b in pipelined_batches(bufs, 6, src=0, fill=fill, method=method)]
+            ok &= len(seen) == 6 and all(np.array_equal(seen[i], stream[i * 65536:i * 65536 + seen[i].size])
+                                         for i in range(6))
+            flags = [None] * world
+            dist.all_gather_object(flags, ok)
+            if rank == 0:
+                q.put(all(flags))
         elif mode == "pipelined":
             from extio_sddc_amd.shard import pipelined_batches
             n = 5
@@ -92,12 +121,13 @@ def _worker(rank, world, port, mode, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", ["segments", "channels", "pipelined"])
-def test_two_rank_gloo(mode):
+@pytest.mark.parametrize("world,mode", [(2, "segments"), (2, "channels"), (2, "pipelined"), (2, "bcast-sag"),
+                                        (4, "bcast-sag"), (3, "bcast-sag"), (2, "bcast-bcast")])
+def test_multi_rank_gloo(world, mode):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, mode, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, mode, q)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:

@@ -148,23 +148,29 @@ def test_dropin_per_block_tune_and_rand(tmp_path, oracle, backend, d, nblk, sche
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("d,nblk,fail_after", [(0, 12, 2), (2, 16, 0)])
-def test_dropin_auto_failover_mid_stream(tmp_path, oracle, d, nblk, fail_after):
+@pytest.mark.parametrize("d,nblk,fail_after,sched", [(0, 12, 1, [(4, 1228, 1), (8, 1228, 0)]),
+                                                      (2, 16, 2, [(5, 1228, 1), (10, 1228, 0)])])
+def test_dropin_auto_failover_mid_stream(tmp_path, oracle, d, nblk, fail_after, sched):
     """SDDC_DDC_BACKEND=auto: the GPU handle's (fail_after+1)-th call fails (injected,
     SDDC_DDC_INJECT_FAIL); the worker announces the switch, redoes that batch on a CPU handle
     from the same ring slots and the last block's tail as history, and the output stream is
-    continuous: every block equals the oracle's, across the switch."""
+    continuous: every block equals the oracle's, across the switch.  The rand changes of the
+    schedule cut the stream into at least len(sched) + 1 calls, so the failure lands mid-stream."""
     tb = 1228
     x = make_stream(nblk, "mix")
     fin, fout = tmp_path / "in.bin", tmp_path / "out.bin"
     x[4096:].tofile(fin)
+    spec = ",".join(f"{k}:{t}:{r}" for k, t, r in sched)
     out, err = _run([HARNESS, str(fin), str(nblk), str(d), str(tb), "0", "0", "1.0", str(fout)], "auto",
-                    env={"SDDC_DDC_INJECT_FAIL": str(fail_after)}, stderr=True)
+                    env={"SDDC_DDC_INJECT_FAIL": str(fail_after), "R2IQ_SCHEDULE": spec}, stderr=True)
     assert "continuing on the CPU" in err, err
     y = np.fromfile(fout, np.float32).view(np.complex64)
-    ref = oracle.r2iq(x, nblk, d, tb)
-    assert y.size == ref.size
-    assert oracle.max_rel_err(y, ref) <= TOL
+    per = 32768 >> d
+    assert y.size == nblk * per
+    bounds = [(0, tb, 0)] + list(sched) + [(nblk, None, None)]
+    for (a, t, r), (b, _, _) in zip(bounds[:-1], bounds[1:]):
+        ref = oracle.r2iq(x[a * 65536: 4096 + b * 65536], b - a, d, t, False, r)
+        assert oracle.max_rel_err(y[a * per: b * per], ref) <= TOL, (a, b)
 
 
 def test_dropin_auto_without_gpu_uses_cpu(tmp_path, oracle):
