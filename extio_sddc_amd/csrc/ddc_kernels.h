@@ -1,4 +1,5 @@
-// ddc_kernels.h — internal (C++) interface between the runtime and the HIP kernels.
+// ddc_kernels.h — internal (C++) interface between the runtime and the HIP kernels of the
+// product library.  The A/B variant kernels live in libsddc_ddc_variants.so (variants/).
 #pragma once
 
 #include <hip/hip_runtime_api.h>
@@ -20,14 +21,9 @@ struct KernelTables {
     const float2 *tw_q1[7] = {};       // [15][S]:  W_{16S}^{s r}   inverse pass 1, S = NS of that pass
     const float2 *rec_f = nullptr;     // [2][256]: W_4096^{j}, W_4096^{4j}  forward pass 2 recurrence
     const float2 *rec_i[7] = {};       // [2][256]: W_N^{j}, W_N^{4j}        inverse pass 2 (N >= 512)
-    const float2 *twt_f = nullptr;     // [15][256]: W_4096^{j r}   forward pass 2 twiddles (table form)
-    const float2 *twt_i[7] = {};       // [15][N/16]: W_N^{j r}     inverse pass 2 twiddles (N >= 512)
-    const float2 *twf64 = nullptr;     // [64][64]: W_4096^{L q} at [q][L]  wave kernel F1 twiddles (d = 0)
+    const float2 *twf64 = nullptr;     // [64][64]: W_4096^{L q} at [q][L]  wave kernel F1 twiddles (d = 0,
+                                       // libsddc_ddc_variants.so)
 };
-
-// v1: one workgroup per frame (kept as a reference variant for A/B timing)
-hipError_t launch_frames(const KernelTables &t, int d, const int16_t *d_in, int nblk, float *d_out,
-                         int tunebin, int lsb, int rand, hipStream_t s);
 
 // v2 (default): persistent workgroups, input prefetch, swizzled LDS.  pq: the split x filter
 // coefficients of (d, tunebin), HALF >> d float4, built by launch_build_split_filter.
@@ -38,25 +34,6 @@ hipError_t launch_frames_persistent(const KernelTables &t, int d, const int16_t 
                                     int cs16, float cs16_scale, const float2 *nco_starts,
                                     const float2 *nco_trig, int device, hipStream_t s);
 hipError_t launch_build_split_filter(const KernelTables &t, int d, int tunebin, float4 *pq, hipStream_t s);
-// d = 0 only: the persistent kernel with two frames in flight per workgroup (forward of frame
-// f and inverse of frame f - 1 share each LDS exchange); same arguments and tables.
-hipError_t launch_frames_pipelined(const KernelTables &t, const int16_t *d_in, int nblk, void *d_out,
-                                   const float4 *pq, int tunebin, int lsb, int rand, int cs16, float cs16_scale,
-                                   const float2 *nco_starts, const float2 *nco_trig, int device, hipStream_t s);
-// d = 0 only: radix 8, 512 threads per frame (8 points per thread); same arguments and tables.
-hipError_t launch_frames_r8(const KernelTables &t, const int16_t *d_in, int nblk, void *d_out, const float4 *pq,
-                            int tunebin, int lsb, int rand, int cs16, float cs16_scale, const float2 *nco_starts,
-                            const float2 *nco_trig, int device, hipStream_t s);
-
-// d = 0 wave kernel (ddc_wave.hip): one wave64 per frame, 64 points per lane.  pqW (4096
-// float4) and twI (4096 float2) are its per-tunebin tables, built by launch_build_wave_tables.
-hipError_t launch_build_wave_tables(const KernelTables &t, int tunebin, float4 *pqW, float2 *twI, hipStream_t s);
-hipError_t launch_frames_wave(const KernelTables &t, const int16_t *d_in, int nblk, void *d_out,
-                              const float4 *pqW, const float2 *twI, int tunebin, int lsb, int rand, int cs16,
-                              float cs16_scale, const float2 *nco_starts, const float2 *nco_trig, int device,
-                              hipStream_t s);
-
-int channels_per_group(int d, int nch);
 
 // many-channel v2 (d = 4..6): persistent, forward once per (frame, 128-channel chunk)
 // stride: scalar components (float or int16) per channel row; cs16 as above.  d_windows:
@@ -75,10 +52,6 @@ hipError_t launch_channels_p(const KernelTables &t, int d, const int16_t *d_in, 
                              float2 *d_scratch, int scratch_rows, int device, hipStream_t s);
 // host: the compact windows of every chunk; false if a chunk's window does not fit
 bool channel_windows(int d, const int *tunebins, int nch, int2 *windows);
-
-hipError_t launch_channels(const KernelTables &t, int d, const int16_t *d_in, int nblk,
-                           const int *d_tunebins, int nch, void *d_out, size_t stride,
-                           int lsb, int rand, int cs16, float cs16_scale, hipStream_t s);
 
 // batched FFTs (fft_batch.hip, include/sddc_fft.h); fft_prepare fills the device's twiddle
 // table once (synchronises s the first time)

@@ -5,6 +5,7 @@
 // (here: twiddle tables), the tune bin and the stream history.  A GPU handle's compute
 // calls go to the gfx950 kernels only (no fallback); a handle created on
 // SDDC_DDC_DEVICE_CPU holds the AVX2 backend (cpu/r2iq_cpu.h) instead and never calls HIP.
+#include <dlfcn.h>
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
@@ -27,6 +28,7 @@
 #include "sddc_fft.h"
 #include "sddc_ddc.h"
 #include "sddc_ddc_internal.h"
+#include "variants/variants_api.h"
 
 namespace {
 
@@ -121,6 +123,38 @@ struct Readers {
         v.clear();
     }
 };
+
+// The A/B variant kernels (variants/variants_api.h) live in libsddc_ddc_variants.so next to
+// this library; it is loaded the first time a handle selects a variant.
+std::once_flag g_variants_once;
+const sddc_variants_api *g_variants = nullptr;
+std::string g_variants_err;
+
+const sddc_variants_api *variants()
+{
+    std::call_once(g_variants_once, [] {
+        std::string path = "libsddc_ddc_variants.so";
+        Dl_info info;
+        if (dladdr(reinterpret_cast<void *>(&sddc_ddc_abi_version), &info) && info.dli_fname) {
+            const std::string self = info.dli_fname;
+            const size_t slash = self.find_last_of('/');
+            if (slash != std::string::npos) path = self.substr(0, slash + 1) + path;
+        }
+        void *lib = dlopen(path.c_str(), RTLD_NOW | RTLD_LOCAL);
+        if (!lib) {
+            g_variants_err = dlerror();
+            return;
+        }
+        auto get = reinterpret_cast<const sddc_variants_api *(*)()>(dlsym(lib, "sddc_variants_get"));
+        const sddc_variants_api *api = get ? get() : nullptr;
+        if (!api || api->version != SDDC_VARIANTS_API_VERSION) {
+            g_variants_err = path + ": no sddc_variants_get of version " + std::to_string(SDDC_VARIANTS_API_VERSION);
+            return;
+        }
+        g_variants = api;
+    });
+    return g_variants;
+}
 
 }  // namespace
 
@@ -304,10 +338,7 @@ int sddc_ddc_create(float gain, int device, sddc_ddc_t **out)
     const size_t o_twf64 = put(64 * 64);   // wave kernel F1 twiddles W_4096^{L q} at [q][L]
     for (int q = 0; q < 64; q++)
         for (int L = 0; L < 64; L++) host[o_twf64 + 64 * q + L] = W((double)((L * q) & 4095), 4096);
-    const size_t o_twtf = put(15 * 256);
-    for (int r = 1; r < 16; r++)
-        for (int j = 0; j < 256; j++) host[o_twtf + (r - 1) * 256 + j] = W((double)j * r, 4096);
-    size_t o_hsel[SDDC_DDC_NDEC], o_q1[SDDC_DDC_NDEC], o_reci[SDDC_DDC_NDEC], o_twti[SDDC_DDC_NDEC];
+    size_t o_hsel[SDDC_DDC_NDEC], o_q1[SDDC_DDC_NDEC], o_reci[SDDC_DDC_NDEC];
     std::vector<std::complex<double>> H(SDDC_DDC_HALF_FFT);
     for (int d = 0; d < SDDC_DDC_NDEC; d++) {
         const int mfft = SDDC_DDC_HALF_FFT >> d;
@@ -326,14 +357,11 @@ int sddc_ddc_create(float gain, int device, sddc_ddc_t **out)
             for (int s = 0; s < S; s++) host[o_q1[d] + (r - 1) * S + s] = W((double)s * r, 16.0 * S);
         // inverse pass-2 recurrence bases W_N^j, W_N^{4j}, j < N/16 (mfft >= 512)
         o_reci[d] = put(2 * 256);
-        o_twti[d] = put(15 * (size_t)(mfft >= 512 ? mfft / 16 : 1));
         if (mfft >= 512) {
             for (int j = 0; j < mfft / 16; j++) {
                 host[o_reci[d] + j] = W(j, mfft);
                 host[o_reci[d] + 256 + j] = W(4.0 * j, mfft);
             }
-            for (int r = 1; r < 16; r++)
-                for (int j = 0; j < mfft / 16; j++) host[o_twti[d] + (r - 1) * (mfft / 16) + j] = W((double)j * r, mfft);
         }
     }
     const size_t ntab = host.size();
@@ -351,13 +379,11 @@ int sddc_ddc_create(float gain, int device, sddc_ddc_t **out)
     h->tables.post8192 = T + o_post;
     h->tables.tw_p1 = T + o_p1;
     h->tables.rec_f = T + o_recf;
-    h->tables.twt_f = T + o_twtf;
     h->tables.twf64 = T + o_twf64;
     for (int d = 0; d < SDDC_DDC_NDEC; d++) {
         h->tables.hsel[d] = T + o_hsel[d];
         h->tables.tw_q1[d] = T + o_q1[d];
         h->tables.rec_i[d] = T + o_reci[d];
-        h->tables.twt_i[d] = T + o_twti[d];
     }
     *out = h;
     return SDDC_OK;
@@ -535,11 +561,12 @@ static hipError_t stage_nco(sddc_ddc_t *h, int nblk, hipStream_t s)
 
 static hipError_t launch_single(sddc_ddc_t *h, const int16_t *d_in, int nblk, void *d_out, hipStream_t s)
 {
+    const sddc_variants_api *V = h->variant ? variants() : nullptr;   // set_variant checked it loads
     if (h->variant == 1) {
         // the v1 reference variant has neither the NCO nor the CS16 stage
         if (h->nco_fc != 0.f || h->out_fmt != SDDC_DDC_FMT_CF32) return hipErrorNotSupported;
-        return sddc::launch_frames(h->tables, h->d, d_in, nblk, static_cast<float *>(d_out), h->tunebin, h->lsb,
-                                   h->rand, s);
+        return V->frames_v1(h->tables, h->d, d_in, nblk, static_cast<float *>(d_out), h->tunebin, h->lsb, h->rand,
+                            s);
     }
     const bool nco = h->nco_fc != 0.f;
     if (nco) {
@@ -553,11 +580,11 @@ static hipError_t launch_single(sddc_ddc_t *h, const int16_t *d_in, int nblk, vo
         if (h->wave_tb != h->tunebin) {
             hipError_t e = h->readers.order_before(s);   // launches on other streams may still read them
             if (e != hipSuccess) return e;
-            e = sddc::launch_build_wave_tables(h->tables, h->tunebin, pqW, twI, s);
+            e = V->build_wave_tables(h->tables, h->tunebin, pqW, twI, s);
             if (e != hipSuccess) return e;
             h->wave_tb = h->tunebin;
         }
-        hipError_t e = sddc::launch_frames_wave(
+        hipError_t e = V->frames_wave(
             h->tables, d_in, nblk, d_out, pqW, twI, h->tunebin, h->lsb, h->rand, h->out_fmt == SDDC_DDC_FMT_CS16,
             h->cs16_scale, nco ? h->d_nco + sddc::FineTune::kTable : nullptr, nco ? h->d_nco : nullptr, h->device, s);
         if (e != hipSuccess) return e;
@@ -573,10 +600,10 @@ static hipError_t launch_single(sddc_ddc_t *h, const int16_t *d_in, int nblk, vo
     }
     const float2 *nco_starts = nco ? h->d_nco + sddc::FineTune::kTable : nullptr, *nco_trig = nco ? h->d_nco : nullptr;
     hipError_t e = h->d == 0 && h->variant == 5
-        ? sddc::launch_frames_r8(h->tables, d_in, nblk, d_out, h->d_pq, h->tunebin, h->lsb, h->rand,
+        ? V->frames_r8(h->tables, d_in, nblk, d_out, h->d_pq, h->tunebin, h->lsb, h->rand,
                                  h->out_fmt == SDDC_DDC_FMT_CS16, h->cs16_scale, nco_starts, nco_trig, h->device, s)
         : h->d == 0 && h->variant == 4
-        ? sddc::launch_frames_pipelined(h->tables, d_in, nblk, d_out, h->d_pq, h->tunebin, h->lsb, h->rand,
+        ? V->frames_pipelined(h->tables, d_in, nblk, d_out, h->d_pq, h->tunebin, h->lsb, h->rand,
                                         h->out_fmt == SDDC_DDC_FMT_CS16, h->cs16_scale, nco_starts, nco_trig,
                                         h->device, s)
         : sddc::launch_frames_persistent(h->tables, h->d, d_in, nblk, d_out, h->d_pq, h->tunebin, h->lsb, h->rand,
@@ -615,6 +642,9 @@ int sddc_ddc_set_fine_tune(sddc_ddc_t *h, float relative_freq)
 int sddc_ddc_internal_set_variant(sddc_ddc_t *h, int variant)
 {
     if (!h || variant < 0 || variant > 5 || variant == 2) return fail(SDDC_ERR_ARG, "bad variant");
+    if (h->cpu) return fail(SDDC_ERR_STATE, "kernel variants are GPU-only");
+    if (variant && !variants())
+        return fail(SDDC_ERR_STATE, "variant %d needs libsddc_ddc_variants.so: %s", variant, g_variants_err.c_str());
     std::lock_guard<std::mutex> lk(h->mu);
     h->variant = variant;
     return SDDC_OK;
@@ -716,7 +746,7 @@ int sddc_ddc_process_channels_device(sddc_ddc_t *h, const int16_t *d_in, int nbl
                                         h->lsb, h->rand, cs16, h->cs16_scale, h->d_chscratch, h->chscratch_rows,
                                         h->device, s));
     else
-        HIP_TRY(sddc::launch_channels(h->tables, h->d, d_in, nblk, h->d_tunebins, nch, d_out, out_stride,
+        HIP_TRY(variants()->channels_v1(h->tables, h->d, d_in, nblk, h->d_tunebins, nch, d_out, out_stride,
                                       h->lsb, h->rand, cs16, h->cs16_scale, s));
     HIP_TRY(h->ch_readers.record(s));
     return SDDC_OK;

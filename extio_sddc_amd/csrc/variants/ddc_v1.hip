@@ -18,7 +18,7 @@
 
 #include "fft_device.hpp"
 #include "ddc_device_io.hpp"
-#include "ddc_kernels.h"
+#include "variants_api.h"
 
 namespace sddc {
 

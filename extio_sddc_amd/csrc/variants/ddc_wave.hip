@@ -28,7 +28,7 @@
 // (consecutive frames share 2048 samples, which then come from the same CU's L2).
 #include <hip/hip_runtime.h>
 
-#include "ddc_kernels.h"
+#include "variants_api.h"
 #include "fft_device.hpp"
 #include "ddc_device_io.hpp"
 

@@ -94,3 +94,18 @@ def test_null_handle_errors(ddc_lib):
     assert ddc_lib.sddc_ddc_process_host(None, None, 1, None) == -1
     assert ddc_lib.sddc_ddc_destroy(None) == 0
     assert ddc_lib.sddc_ddc_kaiser(0, 120.0, 0.4, 0.5, None) > 0
+
+
+def test_variant_kernels_live_outside_the_product_library(ddc_lib):
+    """The measured-slower A/B kernels are built into libsddc_ddc_variants.so, not into the
+    product library (which loads them only when a handle selects a variant)."""
+    import subprocess
+    from extio_sddc_amd._lib import LIB_PATH
+    var = os.path.join(os.path.dirname(LIB_PATH), "libsddc_ddc_variants.so")
+    assert os.path.exists(var)
+    prod = subprocess.run(["nm", "-C", LIB_PATH], capture_output=True, text=True).stdout
+    vsym = subprocess.run(["nm", "-C", "-D", "--defined-only", var], capture_output=True, text=True).stdout
+    for k in ("r2iq_pipe_kernel", "r2iq_r8_kernel", "r2iq_wave_kernel", "r2iq_frame_kernel"):
+        assert k not in prod, k
+    assert "r2iq_persistent_kernel" in prod
+    assert "sddc_variants_get" in vsym

@@ -1,8 +1,8 @@
 """Seeded random parity sweep on a real MI355X (pytest -m gpu): 48 configurations drawn from
 d in 0..6, any legal tune bin (multiple of 4, the setFreqOffset grid, fft_mt_r2iq.cpp:104),
 sideband, rand, the synthetic sources and 1..5 blocks, each checked against the f64 oracle.
-At d = 0 the wave kernel (variant 3) and the two-frame pipelined kernel (variant 4) are checked
-on the same case as well.
+At d = 0 the A/B variants of libsddc_ddc_variants.so (the wave kernel, variant 3; two frames in
+flight, variant 4; radix 8, variant 5) are checked on the same case as well.
 
 Bar: IQ max-rel-err <= 1e-5 (north_star) for every channel whose output reaches -40 dB of
 full scale; a channel below that is "leakage-only" and its error is measured against the -40 dB

@@ -1,7 +1,7 @@
 """The alternative d = 0 kernels against the oracle and against the default persistent-workgroup
-kernel (variant 0), on a real MI355X (pytest -m gpu): the wave kernel (ddc_wave.hip, internal
-variant 3) and the two-frames-in-flight persistent kernel (ddc_persistent.hip
-r2iq_pipe_kernel, variant 4).
+kernel (variant 0), on a real MI355X (pytest -m gpu): the wave kernel (variants/ddc_wave.hip,
+internal variant 3) and the two-frames-in-flight persistent kernel (variants/ddc_variants.hip
+r2iq_pipe_kernel, variant 4), both in libsddc_ddc_variants.so (marker: variants).
 
 Cases specific to their layouts: every tune-bin class of the wave kernel's per-lane tables
 (bins whose mirror is in lane 0 / lane 32, zero-filled bins below 0 and above 4095), sideband /
@@ -18,7 +18,7 @@ import pytest
 
 from extio_sddc_amd.synth import make_stream
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.variants]
 
 TOL = 1e-5
 VARIANTS = [3, 4, 5]
