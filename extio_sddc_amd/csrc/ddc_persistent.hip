@@ -25,6 +25,13 @@
 namespace sddc {
 namespace {
 
+#ifndef SDDC_XRD
+#define SDDC_XRD 0
+#endif
+// one exchange read; SDDC_XRD = 1 keeps every read a separate ds_read_b64 (the compiler would
+// pair r, r + 1 into ds_read2st64_b64, 8 LDS cycles per pair instead of 2 + 2)
+#define XRD(dst, expr) do { dst = (expr); if constexpr (SDDC_XRD) asm volatile("" ::: "memory"); } while (0)
+
 template <int D, bool RAND, bool NCO, bool CS16>
 __global__ __launch_bounds__(NT, 2) void r2iq_persistent_kernel(
     const int *__restrict__ in32, void *__restrict__ out, int nframes,
@@ -97,7 +104,7 @@ __global__ __launch_bounds__(NT, 2) void r2iq_persistent_kernel(
         {
             float2 a[16];
 #pragma unroll
-            for (int r = 0; r < 16; r++) a[r] = w0[sT + NT * r];
+            for (int r = 0; r < 16; r++) XRD(a[r], w0[sT + NT * r]);
 #pragma unroll
             for (int r = 1; r < 16; r++)
                 a[r] = TW<-1>(a[r], twl[(r - 1) * 16 + x15]);
@@ -114,7 +121,7 @@ __global__ __launch_bounds__(NT, 2) void r2iq_persistent_kernel(
         {
             float2 a[16];
 #pragma unroll
-            for (int r = 0; r < 16; r++) a[r] = w1[sT + NT * r];
+            for (int r = 0; r < 16; r++) XRD(a[r], w1[sT + NT * r]);
             twiddle_rec16<-1>(a, fw1, fw4);
             dft16<-1>(a, v);
         }
@@ -164,7 +171,7 @@ __global__ __launch_bounds__(NT, 2) void r2iq_persistent_kernel(
                 float2 a[16];
                 if constexpr (NB == NT) {
 #pragma unroll
-                    for (int r = 0; r < 16; r++) a[r] = w1[sT + NT * r];
+                    for (int r = 0; r < 16; r++) XRD(a[r], w1[sT + NT * r]);
                 } else {
 #pragma unroll
                     for (int r = 0; r < 16; r++) a[r] = w1[swz(t + NB * r)];
@@ -192,7 +199,7 @@ __global__ __launch_bounds__(NT, 2) void r2iq_persistent_kernel(
                 float2 a[16];
                 if constexpr (NB == NT) {
 #pragma unroll
-                    for (int r = 0; r < 16; r++) a[r] = w0[sT + NT * r];
+                    for (int r = 0; r < 16; r++) XRD(a[r], w0[sT + NT * r]);
                 } else {
 #pragma unroll
                     for (int r = 0; r < 16; r++) a[r] = w0[swz(t + NB * r)];
