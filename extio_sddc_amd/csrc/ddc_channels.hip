@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "ddc_kernels.h"
 #include "fft_device.hpp"
@@ -37,6 +38,9 @@ __device__ __forceinline__ int swz(int e) { return e ^ ((e >> 4) & 15); }
 
 #ifndef SDDC_CH_NT
 #define SDDC_CH_NT 1          // non-temporal IQ stores
+#endif
+#ifndef SDDC_CH_STAGE
+#define SDDC_CH_STAGE 1       // d = 5, 6: stage the IQ through the channel slices, 16-B stores
 #endif
 #ifndef SDDC_CH_WAVESYNC
 #define SDDC_CH_WAVESYNC 1   // the per-channel exchange is wave-local: order it within the wave only
@@ -104,7 +108,7 @@ __device__ __forceinline__ float2 split2(float2 zk, float2 zc, float2 wk)
 // goes into a window xw with N/2 zeros either side, so every channel bin, in band or not, reads
 // xw[bin - lo + N/2] without a range test; the per-channel slices reuse the transform buffer
 // (3 workgroups per CU).  Otherwise the split is done in place over all 4096 bins.
-template <int D, bool RAND, bool CS16, bool COMPACT>
+template <int D, bool RAND, bool CS16, bool COMPACT, bool STAGE_OK>
 __global__ __launch_bounds__(NT, 2) void r2iq_channels_v2_kernel(
     const int *__restrict__ in32, void *__restrict__ out, size_t stride, int nframes,
     const int *__restrict__ tunebins, int nch, const float2 *__restrict__ tw_p1,
@@ -117,6 +121,8 @@ __global__ __launch_bounds__(NT, 2) void r2iq_channels_v2_kernel(
     constexpr int G = NT / TPC;          // channels in flight
     constexpr int RB = N / 16;           // pass-B radix
     constexpr int BPT = 16 / TPC;        // pass-B butterflies per thread
+    // d = 5, 6: stage the stores through LDS (needs 16-B aligned channel rows: STAGE_OK)
+    constexpr bool STAGE = SDDC_CH_STAGE && STAGE_OK && N < 256;
 
     static_assert(G * N == HALF, "per-channel slices fill exactly one transform buffer");
     __shared__ __attribute__((aligned(16))) float2 zbuf[COMPACT ? HALF + ZC_MAX + N : 2 * HALF];
@@ -266,7 +272,70 @@ __global__ __launch_bounds__(NT, 2) void r2iq_channels_v2_kernel(
             }
             channel_sync();
             // pass B: radix-RB Stockham step (NS = 16), twiddles W_N^{j q} = W_256^{(256/N) j q}
-            if (cok) {
+            if constexpr (STAGE) {
+                // N < 256: a channel's TPC lanes hold only TPC * 8 B (32 B at d = 6) of each output
+                // row, so direct stores write 32-byte pieces.  Instead the outputs go back into the
+                // channel's LDS slice in stream order, and the wave stores its channels' kept runs
+                // 16 B per lane, consecutive lanes on consecutive bytes: whole lines.
+                float2 y[BPT][RB];
+#pragma unroll
+                for (int b = 0; b < BPT; b++) {
+                    const int j = l + TPC * b;
+                    float2 a[RB];
+#pragma unroll
+                    for (int q = 0; q < RB; q++) a[q] = wg[swz(j + 16 * q)];
+#pragma unroll
+                    for (int q = 1; q < RB; q++) a[q] = cmulc(a[q], twl[((256 / N) * q - 1) * 16 + j]);
+                    dft<RB, +1>(a, y[b]);
+                }
+                channel_sync();   // every lane of the wave has read its slice
+                const int sw = (g * TPC) & 12;   // keeps pairs (2p, 2p + 1) adjacent; conflict-free writes
+#pragma unroll
+                for (int b = 0; b < BPT; b++)
+#pragma unroll
+                    for (int q = 0; q < RB; q++) wg[(l + TPC * b + 16 * q) ^ sw] = flip(y[b][q], oa.lsbmask);
+                channel_sync();
+                constexpr int CW = 64 / TPC;                          // channels per wave
+                const int lane = t & 63, cw0 = cg + (g & ~(CW - 1)); // the wave's first channel
+                const float2 *slices = work + (g & ~(CW - 1)) * N;
+                const int n0 = k == 0 ? N / 4 : 0;                    // first kept output of the frame
+                const int o0 = k == 0 ? 0 : N / 2 + (3 * N / 4) * (k - 1);
+                auto run = [&](auto kept) {
+                    constexpr int K = decltype(kept)::value;          // kept outputs per channel
+                    constexpr int PER = CS16 ? 4 : 2;                 // complex per 16-B piece
+                    constexpr int NP = K / PER;
+#pragma unroll
+                    for (int e0 = 0; e0 < CW * NP; e0 += 64) {
+                        const int e = e0 + lane;
+                        const int cl = e / NP, pc = e - cl * NP;
+                        const int c = cw0 + cl;
+                        if (e >= CW * NP || c >= cend) continue;
+                        const int swc = (((g & ~(CW - 1)) + cl) * TPC) & 12;
+                        const float2 *src = slices + cl * N;
+                        const int n = n0 + PER * pc;
+                        const float4 p0 = *reinterpret_cast<const float4 *>(src + (n ^ swc));
+                        char *ob = static_cast<char *>(out) +
+                                   ((size_t)c * stride + (size_t)blk * 8 * N + o0 + (n - n0)) * out_bytes<CS16>();
+                        if constexpr (CS16) {
+                            const float4 p1 = *reinterpret_cast<const float4 *>(src + ((n + 2) ^ swc));
+                            u32x4 v;
+                            v.x = cs16_pack(make_float2(p0.x, p0.y), oa.scale);
+                            v.y = cs16_pack(make_float2(p0.z, p0.w), oa.scale);
+                            v.z = cs16_pack(make_float2(p1.x, p1.y), oa.scale);
+                            v.w = cs16_pack(make_float2(p1.z, p1.w), oa.scale);
+                            __builtin_nontemporal_store(v, reinterpret_cast<u32x4 *>(ob));
+                        } else {
+                            typedef float f4x __attribute__((ext_vector_type(4)));
+                            const f4x v = {p0.x, p0.y, p0.z, p0.w};
+                            __builtin_nontemporal_store(v, reinterpret_cast<f4x *>(ob));
+                        }
+                    }
+                };
+                if (k == 0)
+                    run(std::integral_constant<int, N / 2>{});
+                else
+                    run(std::integral_constant<int, 3 * N / 4>{});
+            } else if (cok) {
                 char *ob = static_cast<char *>(out) + ((size_t)c * stride + (size_t)blk * 8 * N) * out_bytes<CS16>();
                 auto put = [&](int idx, float2 o) {   // streaming (nt) stores, as the single-channel kernel's
                     if constexpr (CS16) {
@@ -525,7 +594,7 @@ __global__ __launch_bounds__(NT, L2X2 ? SDDC_CHP_WAVES : 2) void r2iq_channels_p
     }
 }
 
-int g_occ[3][8] = {};
+int g_occ[3][16] = {};
 int g_occ_p[4][8] = {};
 int g_cus = 0;
 
@@ -544,11 +613,11 @@ struct ChLaunch {
     hipStream_t s;
 };
 
-template <int D, bool RAND, bool CS16, bool COMPACT>
+template <int D, bool RAND, bool CS16, bool COMPACT, bool STAGE_OK>
 hipError_t launch_v(const KernelTables &t, const ChLaunch &L)
 {
-    auto kern = r2iq_channels_v2_kernel<D, RAND, CS16, COMPACT>;
-    int &occ = g_occ[D - 4][(RAND ? 4 : 0) + (CS16 ? 2 : 0) + (COMPACT ? 1 : 0)];
+    auto kern = r2iq_channels_v2_kernel<D, RAND, CS16, COMPACT, STAGE_OK>;
+    int &occ = g_occ[D - 4][(STAGE_OK ? 8 : 0) + (RAND ? 4 : 0) + (CS16 ? 2 : 0) + (COMPACT ? 1 : 0)];
     if (occ == 0) {
         int nb = 0;
         hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, NT, 0);
@@ -567,10 +636,19 @@ hipError_t launch_v(const KernelTables &t, const ChLaunch &L)
     return hipGetLastError();
 }
 
+template <int D, bool RAND, bool CS16, bool COMPACT>
+hipError_t launch_s(const KernelTables &t, const ChLaunch &L)
+{
+    // the staged 16-B stores of d = 5, 6 need every channel row 16-B aligned
+    const size_t row = L.stride * (CS16 ? 2 : 4);   // bytes (stride counts components)
+    const bool al = D >= 5 && ((uintptr_t)L.d_out & 15) == 0 && (L.nch == 1 || (row & 15) == 0);
+    return al ? launch_v<D, RAND, CS16, COMPACT, true>(t, L) : launch_v<D, RAND, CS16, COMPACT, false>(t, L);
+}
+
 template <int D, bool RAND, bool CS16>
 hipError_t launch_c(const KernelTables &t, const ChLaunch &L)
 {
-    return L.windows ? launch_v<D, RAND, CS16, true>(t, L) : launch_v<D, RAND, CS16, false>(t, L);
+    return L.windows ? launch_s<D, RAND, CS16, true>(t, L) : launch_s<D, RAND, CS16, false>(t, L);
 }
 
 template <int D>
