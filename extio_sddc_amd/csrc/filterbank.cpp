@@ -3,7 +3,7 @@
 // Restates the reference's Kaiser-windowed sinc low-pass (Core/fir.cpp:7-105)
 // and the per-decimation filter bank (Core/fft_mt_r2iq.cpp:163-208).  The Kaiser
 // arithmetic keeps fir.cpp's float operation order so the taps are bit-identical
-// (tests/test_filterbank.py pins them against the reference's own fir.cpp built in
+// (tests/test_capi_cpu.py pins them, through the C ABI, to the reference's own fir.cpp built in
 // oracle/_ref and the committed fixture tests/golden/kaiser_taps.json).  Compile
 // with -ffp-contract=off.  H_d = FFT4096 of the taps is evaluated in double here
 // (the reference does it with a float FFTW plan) and rounded once to float.
