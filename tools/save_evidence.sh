@@ -7,7 +7,7 @@ R=$(cd "$(dirname "$0")/.." && pwd)
 S=$R/gpurun_out/$1; D=$R/profiles/$2
 mkdir -p $D
 tail -n 1 $S/bench.log > $D/bench_line.json
-tail -n 1 $S/trace.log > $D/bench_line_traced.json
+grep -o "{\"metric.*" $S/trace.log > $D/bench_line_traced.json
 cp $S/trace/run_kernel_stats.csv $D/bench_kernel_stats.csv
 grep -v "^\s*$" $S/pytest_gpu.log | tail -n 5 > $D/pytest_gpu.txt
 cp $S/smoke.log $D/smoke.txt
