@@ -37,10 +37,22 @@ template <int D, bool RAND, bool NCO, bool CS16>
 __global__ __launch_bounds__(NT, 2) void r2iq_persistent_kernel(
     const int *__restrict__ in32, void *__restrict__ out, int nframes,
     const float2 *__restrict__ tw_p1, const float2 *__restrict__ tw_q1,
-    const float2 *__restrict__ rec_f, const float2 *__restrict__ rec_i,
+    const float2 *__restrict__ rec_f, const float2 *__restrict__ rec_i, const float2 *__restrict__ tw4096,
     const float4 *__restrict__ pq, int tunebin, OutArgs oa, NcoArgs nco)
 {
     constexpr int N = HALF >> D;
+    // d >= 2 (N <= 1024): the inverse reads only the band [s0, s0 + N) of Z and its mirror
+    // [m0, m0 + N) (s0 = tb - N/2, m0 = 1 - s0 - N, mod 4096).  Forward pass 2 then writes
+    // only the NB of its 16 outputs per thread that can fall in either window: its twiddle
+    // bases are rotated by 256 r0 (r0 = s0 / 256), so output register r holds bin
+    // t + 256 (r + r0) and the band sits in registers 0 .. NB - 1, the mirror in
+    // MREL .. MREL + NB - 1 (mod 16; a uniform test per register).  4 of 16 Z writes per
+    // thread at d >= 4, 6 at d = 3, 10 at d = 2: +5-7 % at d = 3..6, +2-3 % at d = 2
+    // (profiles/r02/ab/prune_d3_6.txt, prune_d2.txt).
+    constexpr bool PRUNE = N <= 1024;
+    constexpr int NB = N >= 512 ? N / 256 + 1 : 2;
+    const int s0 = (tunebin - N / 2) & (HALF - 1), r0 = PRUNE ? s0 >> 8 : 0;
+    const int mrel = ((((1 - s0 - N) & (HALF - 1)) >> 8) - r0) & 15;
     __shared__ __attribute__((aligned(16))) float2 lds[HALF];
     // pass-1 twiddle tables, copied once per workgroup: [15][16] forward, [15][S] inverse
     constexpr int SQ = N >= 512 ? N / 256 : N / 16;
@@ -54,7 +66,8 @@ __global__ __launch_bounds__(NT, 2) void r2iq_persistent_kernel(
     if (f0 >= f1) return;
 
     // per-thread constants, live for the whole frame loop
-    const float2 fw1_ = rec_f[tid], fw4_ = rec_f[NT + tid];
+    const float2 fw1_ = PRUNE ? tw4096[(tid + 256 * r0) & (HALF - 1)] : rec_f[tid];
+    const float2 fw4_ = PRUNE ? tw4096[(4 * tid + 1024 * r0) & (HALF - 1)] : rec_f[NT + tid];
     float2 iw1_ = fw1_, iw4_ = fw4_;
     if constexpr (N >= 512 && N < HALF) {
         if (tid < N / 16) {
@@ -127,8 +140,14 @@ __global__ __launch_bounds__(NT, 2) void r2iq_persistent_kernel(
             dft16<-1>(a, v);
         }
         __syncthreads();
+        if constexpr (PRUNE) {
 #pragma unroll
-        for (int r = 0; r < 16; r++) w0[sT + NT * r] = v[r];   // Z, natural order
+            for (int r = 0; r < 16; r++)   // Z, natural order: the band's and the mirror's registers
+                if (r < NB || ((r - mrel) & 15) < NB) w0[sT + NT * ((r + r0) & 15)] = v[r];
+        } else {
+#pragma unroll
+            for (int r = 0; r < 16; r++) w0[sT + NT * r] = v[r];   // Z, natural order
+        }
         __syncthreads();
 
         if constexpr (N >= 512) {
@@ -305,7 +324,8 @@ hipError_t launch_v(const KernelTables &t, const Launch &L)
     int grid = g_cus * occ;
     if (grid > nframes) grid = nframes;
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), 0, L.s, reinterpret_cast<const int *>(L.d_in),
-                       L.d_out, nframes, t.tw_p1, t.tw_q1[D], t.rec_f, t.rec_i[D], L.pq, L.tunebin, L.oa, L.nco);
+                       L.d_out, nframes, t.tw_p1, t.tw_q1[D], t.rec_f, t.rec_i[D], t.tw4096, L.pq, L.tunebin, L.oa,
+                       L.nco);
     return hipGetLastError();
 }
 
