@@ -39,9 +39,9 @@ __device__ __forceinline__ int swz(int e) { return e ^ ((e >> 4) & 15); }
 #ifndef SDDC_CH_NT
 #define SDDC_CH_NT 1          // non-temporal IQ stores
 #endif
-#ifndef SDDC_CH_STAGE
-#define SDDC_CH_STAGE 1       // d = 5, 6: stage the IQ through the channel slices, 16-B stores
-#endif
+// N <= STAGE_MAX_N (d = 5, 6): stage the IQ through the channel slices, 16-B stores.  At d = 4
+// (128-B pieces already) staging measured 2 % slower for C5 (profiles/r02/channels/ab_stage_d4_*).
+constexpr int STAGE_MAX_N = 128;
 #ifndef SDDC_CH_WAVESYNC
 #define SDDC_CH_WAVESYNC 1   // the per-channel exchange is wave-local: order it within the wave only
 #endif
@@ -122,7 +122,7 @@ __global__ __launch_bounds__(NT, 2) void r2iq_channels_v2_kernel(
     constexpr int RB = N / 16;           // pass-B radix
     constexpr int BPT = 16 / TPC;        // pass-B butterflies per thread
     // d = 5, 6: stage the stores through LDS (needs 16-B aligned channel rows: STAGE_OK)
-    constexpr bool STAGE = SDDC_CH_STAGE && STAGE_OK && N < 256;
+    constexpr bool STAGE = STAGE_OK && N <= STAGE_MAX_N;
 
     static_assert(G * N == HALF, "per-channel slices fill exactly one transform buffer");
     __shared__ __attribute__((aligned(16))) float2 zbuf[COMPACT ? HALF + ZC_MAX + N : 2 * HALF];
@@ -641,7 +641,7 @@ hipError_t launch_s(const KernelTables &t, const ChLaunch &L)
 {
     // the staged 16-B stores of d = 5, 6 need every channel row 16-B aligned
     const size_t row = L.stride * (CS16 ? 2 : 4);   // bytes (stride counts components)
-    const bool al = D >= 5 && ((uintptr_t)L.d_out & 15) == 0 && (L.nch == 1 || (row & 15) == 0);
+    const bool al = (HALF >> D) <= STAGE_MAX_N && ((uintptr_t)L.d_out & 15) == 0 && (L.nch == 1 || (row & 15) == 0);
     return al ? launch_v<D, RAND, CS16, COMPACT, true>(t, L) : launch_v<D, RAND, CS16, COMPACT, false>(t, L);
 }
 
