@@ -85,3 +85,30 @@ def test_registered_direct_dma(torch_dev):
         r.TurnOn()
         y = r.process(inp)                  # staged again after unregistering
     np.testing.assert_array_equal(y.view(np.uint32), ref.view(np.uint32))
+
+
+@pytest.mark.parametrize("d,split", [(0, 3), (2, 40)])
+def test_set_history_continues_stream_on_new_handle(torch_dev, d, split):
+    """sddc_ddc_set_history (the drop-in's failover uses it): a fresh handle given the tail of
+    block split-1 as history continues the stream bit-exactly, whether the first call is one
+    chunk or spans several pipeline chunks; and a GPU handle continues a CPU handle's stream
+    within the parity bar."""
+    from extio_sddc_amd import DEVICE_CPU, R2iq
+    nblk = split + 5
+    x = make_stream(nblk, "mix")
+    with _ddc(d) as r:
+        whole = r.process(x[4096:])
+    per = 32768 >> d
+    with _ddc(d) as r2:
+        r2.setHistory(x[split * BLOCK: split * BLOCK + 4096])
+        tail = r2.process(x[4096 + split * BLOCK:])
+    np.testing.assert_array_equal(tail.view(np.uint32), whole[split * per:].view(np.uint32))
+    with R2iq(gain=1.0, device=DEVICE_CPU) as c:
+        c.setDecimate(d)
+        c.setTuneBin(1024)
+        head = c.process(x[4096:4096 + split * BLOCK])
+    with _ddc(d) as r3:
+        r3.setHistory(x[split * BLOCK: split * BLOCK + 4096])
+        rest = r3.process(x[4096 + split * BLOCK:])
+    y = np.concatenate([head, rest])
+    assert np.max(np.abs(y - whole)) / np.max(np.abs(whole)) <= 1e-5
