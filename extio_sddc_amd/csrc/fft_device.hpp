@@ -106,10 +106,67 @@ __device__ __forceinline__ void dft8(const float2 *v, float2 *o)
     }
 }
 
+#ifndef SDDC_DFT16_FMA
+#define SDDC_DFT16_FMA 1
+#endif
+
+// z (1 + i tau)
+__device__ __forceinline__ float2 rot1(float2 z, float tau)
+{
+    return make_float2(fmaf(-tau, z.y, z.x), fmaf(tau, z.x, z.y));
+}
+// p = a + c z, m = a - c z (real c)
+__device__ __forceinline__ void axpm(float2 a, float c, float2 z, float2 &p, float2 &m)
+{
+    p = make_float2(fmaf(c, z.x, a.x), fmaf(c, z.y, a.y));
+    m = make_float2(fmaf(-c, z.x, a.x), fmaf(-c, z.y, a.y));
+}
+// p = a + DIR i c z, m = a - DIR i c z (real c)
+template <int DIR>
+__device__ __forceinline__ void ajpm(float2 a, float c, float2 z, float2 &p, float2 &m)
+{
+    const float dc = DIR * c;
+    p = make_float2(fmaf(-dc, z.y, a.x), fmaf(dc, z.x, a.y));
+    m = make_float2(fmaf(dc, z.y, a.x), fmaf(-dc, z.x, a.y));
+}
+
 // 16 = 4 x 4: n = 4 n1 + n2, k = k1 + 4 k2
 template <int DIR>
 __device__ __forceinline__ void dft16(const float2 *v, float2 *o)
 {
+#if SDDC_DFT16_FMA
+    // Second-stage twiddles in tangent form, W^m = cos(m th) (1 + i DIR tan(m th)) with
+    // th = 2 pi / 16: each twiddled value enters its radix-4 as a 2-FMA rotation, and the cos
+    // scale rides on the FMA that combines it (the pair W^1 / W^3 of columns 1 and 3 shares
+    // one scale through the ratio cos 3th / cos th = tan th).  144 VALU instead of 156, same
+    // results to float rounding.
+    constexpr float kT1 = 0.41421356237309504880f;   // tan(pi/8) = cos(3pi/8) / cos(pi/8)
+    constexpr float kT3 = 2.41421356237309504880f;   // tan(3pi/8)
+    float2 b[4][4];  // b[n2][k1]
+#pragma unroll
+    for (int n2 = 0; n2 < 4; n2++)
+        dft4<DIR>(v[n2], v[4 + n2], v[8 + n2], v[12 + n2], b[n2][0], b[n2][1], b[n2][2], b[n2][3]);
+    dft4<DIR>(b[0][0], b[1][0], b[2][0], b[3][0], o[0], o[4], o[8], o[12]);
+    float2 t0, t1, p, q;
+    {   // k1 = 1: W^1 b1, W^2 b2, W^3 b3
+        axpm(b[0][1], kR2, rot1(b[2][1], (float)DIR), t0, t1);
+        axpm(rot1(b[1][1], DIR * kT1), kT1, rot1(b[3][1], DIR * kT3), p, q);
+        axpm(t0, kC16_1, p, o[1], o[9]);
+        ajpm<DIR>(t1, kC16_1, q, o[5], o[13]);
+    }
+    {   // k1 = 2: W^2 b1, W^4 b2 = DIR i b2, W^6 b3
+        ajpm<DIR>(b[0][2], 1.f, b[2][2], t0, t1);
+        axpm(rot1(b[1][2], (float)DIR), -1.f, rot1(b[3][2], (float)-DIR), p, q);
+        axpm(t0, kR2, p, o[2], o[10]);
+        ajpm<DIR>(t1, kR2, q, o[6], o[14]);
+    }
+    {   // k1 = 3: W^3 b1, W^6 b2, W^9 b3 = -W^1 b3
+        axpm(b[0][3], -kR2, rot1(b[2][3], (float)-DIR), t0, t1);
+        axpm(rot1(b[1][3], DIR * kT3), -kT3, rot1(b[3][3], DIR * kT1), p, q);
+        axpm(t0, kS16_1, p, o[3], o[11]);
+        ajpm<DIR>(t1, kS16_1, q, o[7], o[15]);
+    }
+#else
     float2 b[4][4];  // b[n2][k1]
 #pragma unroll
     for (int n2 = 0; n2 < 4; n2++)
@@ -126,6 +183,7 @@ __device__ __forceinline__ void dft16(const float2 *v, float2 *o)
 #pragma unroll
     for (int k1 = 0; k1 < 4; k1++)
         dft4<DIR>(b[0][k1], b[1][k1], b[2][k1], b[3][k1], o[k1], o[k1 + 4], o[k1 + 8], o[k1 + 12]);
+#endif
 }
 
 template <int R, int DIR>

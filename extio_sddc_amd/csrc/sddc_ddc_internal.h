@@ -7,7 +7,8 @@ extern "C" {
 /* Select the single-channel kernel: 0 = persistent workgroups (default, ddc_persistent.hip),
  * 1 = one workgroup per frame (v1), 3 = one wave per frame at d = 0 (ddc_wave.hip),
  * 4 = two frames in flight per workgroup at d = 0 (r2iq_pipe_kernel), 5 = radix 8 with 512
- * threads per frame at d = 0 (r2iq_r8_kernel); 3, 4 and 5 run the persistent kernel at d > 0.  Used by tools/ab_kernels.py to time variants in one process. */
+ * threads per frame at d = 0 (r2iq_r8_kernel), 6 = lane pairs, 512 threads per frame at d = 0
+ * (r2iq_pair_kernel); 3..6 run the persistent kernel at d > 0.  Used by tools/ab_kernels.py to time variants in one process. */
 int sddc_ddc_internal_set_variant(sddc_ddc_t *h, int variant);
 #ifdef __cplusplus
 }
