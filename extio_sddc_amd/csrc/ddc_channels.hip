@@ -68,32 +68,6 @@ __device__ __forceinline__ float derand(int v)
     return __int_as_float(__float_as_int(f) ^ (v << 31));   // odd int16 ^ 0xFFFE == -v
 }
 
-template <int DIR>
-__device__ __forceinline__ void twiddle_rec16(float2 *a, float2 w1, float2 w4)
-{
-    if (DIR > 0) {
-        w1.y = -w1.y;
-        w4.y = -w4.y;
-    }
-    const float2 w2 = cmul(w1, w1), w3 = cmul(w2, w1);
-    const float2 w8 = cmul(w4, w4), w12 = cmul(w8, w4);
-    a[1] = cmul(a[1], w1);
-    a[2] = cmul(a[2], w2);
-    a[3] = cmul(a[3], w3);
-    a[4] = cmul(a[4], w4);
-    a[5] = cmul(a[5], cmul(w4, w1));
-    a[6] = cmul(a[6], cmul(w4, w2));
-    a[7] = cmul(a[7], cmul(w4, w3));
-    a[8] = cmul(a[8], w8);
-    a[9] = cmul(a[9], cmul(w8, w1));
-    a[10] = cmul(a[10], cmul(w8, w2));
-    a[11] = cmul(a[11], cmul(w8, w3));
-    a[12] = cmul(a[12], w12);
-    a[13] = cmul(a[13], cmul(w12, w1));
-    a[14] = cmul(a[14], cmul(w12, w2));
-    a[15] = cmul(a[15], cmul(w12, w3));
-}
-
 // 2 X[k] = (Z_k + conj Z_-k) - i W_8192^k (Z_k - conj Z_-k), Z = FFT4096(x_even + i x_odd)
 __device__ __forceinline__ float2 split2(float2 zk, float2 zc, float2 wk)
 {

@@ -186,6 +186,82 @@ __device__ __forceinline__ void dft16(const float2 *v, float2 *o)
 #endif
 }
 
+// a[r] *= W^{r} for r = 1..15 given the forward-direction W^1 and W^4 of this lane
+// (conjugated for DIR = +1).
+#ifndef SDDC_TWREC_CHEB
+#define SDDC_TWREC_CHEB 1
+#endif
+// p = A w, m = A conj(w) for a unit w
+__device__ __forceinline__ void cmul_pm(float2 A, float2 w, float2 &p, float2 &m)
+{
+    const float cx = w.x * A.x, cy = w.x * A.y;
+    p = make_float2(fmaf(-w.y, A.y, cx), fmaf(w.y, A.x, cy));
+    m = make_float2(fmaf(w.y, A.y, cx), fmaf(-w.y, A.x, cy));
+}
+// 2 c a - b (real c2 = 2 c): the three-term recurrence W^{m+n} = 2 cos(n th) W^m - W^{m-n}
+__device__ __forceinline__ float2 cheb(float c2, float2 a, float2 b)
+{
+    return make_float2(fmaf(c2, a.x, -b.x), fmaf(c2, a.y, -b.y));
+}
+template <int DIR>
+__device__ __forceinline__ void twiddle_rec16(float2 *a, float2 w1, float2 w4)
+{
+    if (DIR > 0) {
+        w1.y = -w1.y;
+        w4.y = -w4.y;
+    }
+#if SDDC_TWREC_CHEB
+    // W^8, W^12 as products; W^{4k +- 1} as pairs A W, A conj(W) sharing the products cos * A
+    // (3 ops each); W^2 and W^{4k + 2}, W^15 by one step of the Chebyshev recurrence
+    // W^{m+1} = 2 cos(th) W^m - W^{m-1} (2 FMAs): 38 VALU for the 13 powers instead of 52.
+    // float32 model over all 4096 bases: worst power error 4.6e-7 (rms 7.1e-8) against 3.2e-7
+    // (6.9e-8) for the all-product form; a pure Chebyshev form (28 VALU, 1.3e-6) leaked past the
+    // 1e-5 bar on the out-of-band parity case at d = 4 (profiles/r02/ab/cheb.txt).
+    const float c1 = w1.x + w1.x;
+    const float2 w8 = cmul(w4, w4), w12 = cmul(w8, w4);
+    float2 w3, w5, w7, w9, w11, w13;
+    cmul_pm(w4, w1, w5, w3);
+    cmul_pm(w8, w1, w9, w7);
+    cmul_pm(w12, w1, w13, w11);
+    const float2 w2 = cheb(c1, w1, make_float2(1.f, 0.f)), w6 = cheb(c1, w5, w4);
+    const float2 w10 = cheb(c1, w9, w8), w14 = cheb(c1, w13, w12), w15 = cheb(c1, w14, w13);
+    a[1] = cmul(a[1], w1);
+    a[2] = cmul(a[2], w2);
+    a[3] = cmul(a[3], w3);
+    a[4] = cmul(a[4], w4);
+    a[5] = cmul(a[5], w5);
+    a[6] = cmul(a[6], w6);
+    a[7] = cmul(a[7], w7);
+    a[8] = cmul(a[8], w8);
+    a[9] = cmul(a[9], w9);
+    a[10] = cmul(a[10], w10);
+    a[11] = cmul(a[11], w11);
+    a[12] = cmul(a[12], w12);
+    a[13] = cmul(a[13], w13);
+    a[14] = cmul(a[14], w14);
+    a[15] = cmul(a[15], w15);
+#else
+    // every power at most three products away
+    const float2 w2 = cmul(w1, w1), w3 = cmul(w2, w1);
+    const float2 w8 = cmul(w4, w4), w12 = cmul(w8, w4);
+    a[1] = cmul(a[1], w1);
+    a[2] = cmul(a[2], w2);
+    a[3] = cmul(a[3], w3);
+    a[4] = cmul(a[4], w4);
+    a[5] = cmul(a[5], cmul(w4, w1));
+    a[6] = cmul(a[6], cmul(w4, w2));
+    a[7] = cmul(a[7], cmul(w4, w3));
+    a[8] = cmul(a[8], w8);
+    a[9] = cmul(a[9], cmul(w8, w1));
+    a[10] = cmul(a[10], cmul(w8, w2));
+    a[11] = cmul(a[11], cmul(w8, w3));
+    a[12] = cmul(a[12], w12);
+    a[13] = cmul(a[13], cmul(w12, w1));
+    a[14] = cmul(a[14], cmul(w12, w2));
+    a[15] = cmul(a[15], cmul(w12, w3));
+#endif
+}
+
 template <int R, int DIR>
 __device__ __forceinline__ void dft(const float2 *v, float2 *o)
 {
