@@ -33,6 +33,10 @@ namespace {
 // (profiles/r02/ab/twrd.txt).
 #define XRD(dst, expr) do { dst = (expr); asm volatile("" ::: "memory"); } while (0)
 
+#ifndef SDDC_ZROT
+#define SDDC_ZROT 1
+#endif
+
 template <int D, bool RAND, bool NCO, bool CS16>
 __global__ __launch_bounds__(NT, 2) void r2iq_persistent_kernel(
     const int *__restrict__ in32, void *__restrict__ out, int nframes,
@@ -52,6 +56,13 @@ __global__ __launch_bounds__(NT, 2) void r2iq_persistent_kernel(
     constexpr bool PRUNE = N <= 1024;
     constexpr int NB = N >= 512 ? N / 256 + 1 : 2;
     const int s0 = (tunebin - N / 2) & (HALF - 1), r0 = PRUNE ? s0 >> 8 : 0;
+    // d <= 1: Z is stored rotated by the tune bin, bin j at swz((j - tb) mod 4096), so the
+    // inverse's reads of bins tb + m are sT + 256 r with no wrap (the mirror reads keep theirs).
+    // Forward pass 2 gets it for free: per-lane twiddle bases rotated by 256 zr make output
+    // register r hold bin t + 256 (r + zr), i.e. tb + ((t - tb) mod 256) + 256 r.  d = 0 +1.5-2 %,
+    // d = 1 +1 % (profiles/r02/ab/zrot.txt).
+    constexpr bool ZROT = SDDC_ZROT && !PRUNE;
+    const int zd = tunebin & 255;
     const int mrel = ((((1 - s0 - N) & (HALF - 1)) >> 8) - r0) & 15;
     __shared__ __attribute__((aligned(16))) float2 lds[HALF];
     // pass-1 twiddle tables, copied once per workgroup: [15][16] forward, [15][S] inverse
@@ -66,9 +77,10 @@ __global__ __launch_bounds__(NT, 2) void r2iq_persistent_kernel(
     if (f0 >= f1) return;
 
     // per-thread constants, live for the whole frame loop
-    const float2 fw1_ = PRUNE ? tw4096[(tid + 256 * r0) & (HALF - 1)] : rec_f[tid];
-    const float2 fw4_ = PRUNE ? tw4096[(4 * tid + 1024 * r0) & (HALF - 1)] : rec_f[NT + tid];
-    float2 iw1_ = fw1_, iw4_ = fw4_;
+    const int zr = ZROT ? (tunebin >> 8) + (tid < zd ? 1 : 0) : r0;
+    const float2 fw1_ = PRUNE || ZROT ? tw4096[(tid + 256 * zr) & (HALF - 1)] : rec_f[tid];
+    const float2 fw4_ = PRUNE || ZROT ? tw4096[(4 * tid + 1024 * zr) & (HALF - 1)] : rec_f[NT + tid];
+    float2 iw1_ = ZROT ? rec_f[tid] : fw1_, iw4_ = ZROT ? rec_f[NT + tid] : fw4_;
     if constexpr (N >= 512 && N < HALF) {
         if (tid < N / 16) {
             iw1_ = rec_i[tid];
@@ -144,6 +156,10 @@ __global__ __launch_bounds__(NT, 2) void r2iq_persistent_kernel(
 #pragma unroll
             for (int r = 0; r < 16; r++)   // Z, natural order: the band's and the mirror's registers
                 if (r < NB || ((r - mrel) & 15) < NB) w0[sT + NT * ((r + r0) & 15)] = v[r];
+        } else if constexpr (ZROT) {
+            const int sZ = swz((t - zd) & 255);
+#pragma unroll
+            for (int r = 0; r < 16; r++) w0[sZ + NT * r] = v[r];   // Z, rotated by tb
         } else {
 #pragma unroll
             for (int r = 0; r < 16; r++) w0[sT + NT * r] = v[r];   // Z, natural order
@@ -157,7 +173,8 @@ __global__ __launch_bounds__(NT, 2) void r2iq_persistent_kernel(
             {
                 const int b0 = tunebin + t;                  // bin of r = 0
                 const int sb0 = swz(b0);                     // swz(b0 + 256 r - N w) = sb0 + 256 r - N w
-                const int sc0 = swz(HALF - b0);              // mirror bin, same separability
+                // mirror bin, same separability (rotated storage: HALF - b0 - tb)
+                const int sc0 = ZROT ? swz((HALF - b0 - tunebin) & (HALF - 1)) : swz(HALF - b0);
                 const char *w0b = reinterpret_cast<const char *>(w0);
                 const unsigned sb0b = 8u * (unsigned)sb0, sc0b = 8u * (unsigned)sc0, tb16 = 16u * (unsigned)t;
                 const __amdgpu_buffer_rsrc_t rpq = buf_rsrc(pqz);
@@ -168,7 +185,11 @@ __global__ __launch_bounds__(NT, 2) void r2iq_persistent_kernel(
                     const int sh = NT * r - (wrap ? N : 0);
                     // branch-free: read a valid (wrapped) address, out-of-band bins have P = Q = 0;
                     // byte offsets: the wrap is one AND, the scale folds away
-                    const float2 zk = *reinterpret_cast<const float2 *>(w0b + ((sb0b + 8u * (unsigned)sh) & (8u * HALF - 8u)));
+                    float2 zk;
+                    // unpaired (XRD) at d = 1: +1 %; at d = 0 the clobbers cost 5 % (profiles/r02/ab/zrot.txt)
+                    if constexpr (ZROT && D > 0) XRD(zk, w0[sT + (sh & (HALF - 1))]);
+                    else if constexpr (ZROT) zk = w0[sT + (sh & (HALF - 1))];
+                    else zk = *reinterpret_cast<const float2 *>(w0b + ((sb0b + 8u * (unsigned)sh) & (8u * HALF - 8u)));
                     const float2 zc = *reinterpret_cast<const float2 *>(w0b + ((sc0b - 8u * (unsigned)sh) & (8u * HALF - 8u)));
                     a[r] = split_pq(zk, zc, buf_load16(rpq, tb16, 16u * NT * r));
                 }

@@ -599,7 +599,10 @@ static hipError_t launch_single(sddc_ddc_t *h, const int16_t *d_in, int nblk, vo
         h->pq_tb = h->tunebin;
     }
     const float2 *nco_starts = nco ? h->d_nco + sddc::FineTune::kTable : nullptr, *nco_trig = nco ? h->d_nco : nullptr;
-    hipError_t e = h->d == 0 && h->variant == 6
+    hipError_t e = h->d == 0 && h->variant == 7
+        ? V->frames_inplace(h->tables, d_in, nblk, d_out, h->d_pq, h->tunebin, h->lsb, h->rand,
+                            h->out_fmt == SDDC_DDC_FMT_CS16, h->cs16_scale, nco_starts, nco_trig, h->device, s)
+        : h->d == 0 && h->variant == 6
         ? V->frames_pair(h->tables, d_in, nblk, d_out, h->d_pq, h->tunebin, h->lsb, h->rand,
                          h->out_fmt == SDDC_DDC_FMT_CS16, h->cs16_scale, nco_starts, nco_trig, h->device, s)
         : h->d == 0 && h->variant == 5
@@ -644,7 +647,7 @@ int sddc_ddc_set_fine_tune(sddc_ddc_t *h, float relative_freq)
 /* internal (not in include/sddc_ddc.h): kernel variant for A/B timing, see sddc_ddc_internal.h */
 int sddc_ddc_internal_set_variant(sddc_ddc_t *h, int variant)
 {
-    if (!h || variant < 0 || variant > 6 || variant == 2) return fail(SDDC_ERR_ARG, "bad variant");
+    if (!h || variant < 0 || variant > 7 || variant == 2) return fail(SDDC_ERR_ARG, "bad variant");
     if (h->cpu) return fail(SDDC_ERR_STATE, "kernel variants are GPU-only");
     if (variant && !variants())
         return fail(SDDC_ERR_STATE, "variant %d needs libsddc_ddc_variants.so: %s", variant, g_variants_err.c_str());

@@ -8,7 +8,8 @@ extern "C" {
  * 1 = one workgroup per frame (v1), 3 = one wave per frame at d = 0 (ddc_wave.hip),
  * 4 = two frames in flight per workgroup at d = 0 (r2iq_pipe_kernel), 5 = radix 8 with 512
  * threads per frame at d = 0 (r2iq_r8_kernel), 6 = lane pairs, 512 threads per frame at d = 0
- * (r2iq_pair_kernel); 3..6 run the persistent kernel at d > 0.  Used by tools/ab_kernels.py to time variants in one process. */
+ * (r2iq_pair_kernel), 7 = in-place LDS passes at d = 0 (r2iq_inplace_kernel); 3..7 run the
+ * persistent kernel at d > 0.  Used by tools/ab_kernels.py to time variants in one process. */
 int sddc_ddc_internal_set_variant(sddc_ddc_t *h, int variant);
 #ifdef __cplusplus
 }

@@ -455,7 +455,7 @@ extern "C" const sddc_variants_api *sddc_variants_get(void)
     static const sddc_variants_api api = {
         SDDC_VARIANTS_API_VERSION, sddc::launch_frames,    sddc::launch_channels,    sddc::launch_frames_pipelined,
         sddc::launch_frames_r8,    sddc::launch_build_wave_tables, sddc::launch_frames_wave,
-        sddc::launch_frames_pair,
+        sddc::launch_frames_pair,  sddc::launch_frames_inplace,
     };
     return &api;
 }

@@ -32,6 +32,11 @@ hipError_t launch_frames_pair(const KernelTables &t, const int16_t *d_in, int nb
                               int tunebin, int lsb, int rand, int cs16, float cs16_scale, const float2 *nco_starts,
                               const float2 *nco_trig, int device, hipStream_t s);
 
+// d = 0, in-place LDS passes, 7 barriers per frame (variant 7, ddc_inplace.hip)
+hipError_t launch_frames_inplace(const KernelTables &t, const int16_t *d_in, int nblk, void *d_out, const float4 *pq,
+                                 int tunebin, int lsb, int rand, int cs16, float cs16_scale, const float2 *nco_starts,
+                                 const float2 *nco_trig, int device, hipStream_t s);
+
 // d = 0, one wave64 per frame, 64 points per lane (variant 3, ddc_wave.hip).  pqW (4096
 // float4) and twI (4096 float2) are its per-tunebin tables, built by launch_build_wave_tables.
 hipError_t launch_build_wave_tables(const KernelTables &t, int tunebin, float4 *pqW, float2 *twI, hipStream_t s);
@@ -42,7 +47,7 @@ hipError_t launch_frames_wave(const KernelTables &t, const int16_t *d_in, int nb
 
 }  // namespace sddc
 
-#define SDDC_VARIANTS_API_VERSION 2
+#define SDDC_VARIANTS_API_VERSION 3
 
 extern "C" {
 struct sddc_variants_api {
@@ -54,6 +59,7 @@ struct sddc_variants_api {
     decltype(&sddc::launch_build_wave_tables) build_wave_tables;
     decltype(&sddc::launch_frames_wave) frames_wave;
     decltype(&sddc::launch_frames_pair) frames_pair;
+    decltype(&sddc::launch_frames_inplace) frames_inplace;
 };
 // the table (exported by libsddc_ddc_variants.so, looked up with dlsym)
 const sddc_variants_api *sddc_variants_get(void);

@@ -2,7 +2,7 @@
 d in 0..6, any legal tune bin (multiple of 4, the setFreqOffset grid, fft_mt_r2iq.cpp:104),
 sideband, rand, the synthetic sources and 1..5 blocks, each checked against the f64 oracle.
 At d = 0 the A/B variants of libsddc_ddc_variants.so (the wave kernel, variant 3; two frames in
-flight, variant 4; radix 8, variant 5; lane pairs, variant 6) are checked on the same case as well.
+flight, variant 4; radix 8, variant 5; lane pairs, variant 6; in-place passes, variant 7) are checked on the same case as well.
 
 Bar: IQ max-rel-err <= 1e-5 (north_star) for every channel whose output reaches -40 dB of
 full scale; a channel below that is "leakage-only" and its error is measured against the -40 dB
@@ -75,7 +75,7 @@ def test_random_config_parity(ddc, oracle, H, d, tb, lsb, rand, src, nblk, seed)
     x = make_stream(nblk, src, seed=seed)
     r = oracle.r2iq(x, nblk, d, tb, lsb, rand, H=H)
     d_in = torch.from_numpy(x).to("cuda")
-    for variant in ([0, 3, 4, 5, 6] if d == 0 else [0]):
+    for variant in ([0, 3, 4, 5, 6, 7] if d == 0 else [0]):
         _lib.check(ddc._L.sddc_ddc_internal_set_variant(ddc._h, variant))
         try:
             ddc.setDecimate(d)

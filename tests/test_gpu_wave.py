@@ -21,7 +21,7 @@ from extio_sddc_amd.synth import make_stream
 pytestmark = [pytest.mark.gpu, pytest.mark.variants]
 
 TOL = 1e-5
-VARIANTS = [3, 4, 5, 6]
+VARIANTS = [3, 4, 5, 6, 7]
 
 
 @pytest.fixture(scope="module")
