@@ -36,9 +36,41 @@ namespace {
 #ifndef SDDC_ZROT
 #define SDDC_ZROT 1
 #endif
+// Pass-1 table twiddles at d <= 1: issued in two groups (8 + 7) right behind the data reads, so
+// the products wait on two LDS round trips instead of one per ds_read2 pair (the compiler's own
+// schedule); the kernel is held to 128 VGPRs for it.  d = 0 +1-2.7 %, d = 1 +1 %; one group of
+// 15 spills and loses at every d, and at d >= 2 either form loses 1-5 % (profiles/r02/ab/early.txt).
+#ifndef SDDC_TW_EARLY
+#define SDDC_TW_EARLY 1
+#endif
+
+// a[r] *= tbl[(r - 1) S + j] (conjugated for DIR > 0), r = 1..15.  EARLY: the table reads are
+// issued in two groups (8 + 7) right behind the caller's exchange reads, each group before its
+// products (empty asm with a memory clobber), so the products wait on two LDS round trips; the
+// compiler's own schedule issues one ds_read2 pair at a time and waits lgkmcnt(0) after each.
+template <int DIR, bool EARLY>
+__device__ __forceinline__ void table_twiddle(float2 *a, const float2 *tbl, int S, int j)
+{
+    if constexpr (EARLY) {
+        float2 tw[15];
+#pragma unroll
+        for (int r = 1; r <= 8; r++) tw[r - 1] = tbl[(r - 1) * S + j];
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int r = 1; r <= 8; r++) a[r] = TW<DIR>(a[r], tw[r - 1]);
+#pragma unroll
+        for (int r = 9; r < 16; r++) tw[r - 1] = tbl[(r - 1) * S + j];
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int r = 9; r < 16; r++) a[r] = TW<DIR>(a[r], tw[r - 1]);
+    } else {
+#pragma unroll
+        for (int r = 1; r < 16; r++) a[r] = TW<DIR>(a[r], tbl[(r - 1) * S + j]);
+    }
+}
 
 template <int D, bool RAND, bool NCO, bool CS16>
-__global__ __launch_bounds__(NT, 2) void r2iq_persistent_kernel(
+__global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
     const int *__restrict__ in32, void *__restrict__ out, int nframes,
     const float2 *__restrict__ tw_p1, const float2 *__restrict__ tw_q1,
     const float2 *__restrict__ rec_f, const float2 *__restrict__ rec_i, const float2 *__restrict__ tw4096,
@@ -54,6 +86,7 @@ __global__ __launch_bounds__(NT, 2) void r2iq_persistent_kernel(
     // thread at d >= 4, 6 at d = 3, 10 at d = 2: +5-7 % at d = 3..6, +2-3 % at d = 2
     // (profiles/r02/ab/prune_d3_6.txt, prune_d2.txt).
     constexpr bool PRUNE = N <= 1024;
+    constexpr bool TW_EARLY = SDDC_TW_EARLY && D <= 1;   // (held to 128 VGPRs by the launch bounds)
     constexpr int NB = N >= 512 ? N / 256 + 1 : 2;
     const int s0 = (tunebin - N / 2) & (HALF - 1), r0 = PRUNE ? s0 >> 8 : 0;
     // d <= 1: Z is stored rotated by the tune bin, bin j at swz((j - tb) mod 4096), so the
@@ -131,9 +164,7 @@ __global__ __launch_bounds__(NT, 2) void r2iq_persistent_kernel(
             float2 a[16];
 #pragma unroll
             for (int r = 0; r < 16; r++) XRD(a[r], w0[sT + NT * r]);
-#pragma unroll
-            for (int r = 1; r < 16; r++)
-                a[r] = TW<-1>(a[r], twl[(r - 1) * 16 + x15]);
+            table_twiddle<-1, TW_EARLY>(a, twl, 16, x15);
             dft16<-1>(a, v);
         }
         __syncthreads();
@@ -217,9 +248,7 @@ __global__ __launch_bounds__(NT, 2) void r2iq_persistent_kernel(
 #pragma unroll
                     for (int r = 0; r < 16; r++) a[r] = w1[swz(t + NB * r)];
                 }
-#pragma unroll
-                for (int r = 1; r < 16; r++)
-                    a[r] = TW<+1>(a[r], twl[15 * 16 + (r - 1) * R0 + (t % R0)]);
+                table_twiddle<+1, TW_EARLY>(a, twl + 15 * 16, R0, t % R0);
                 dft16<+1>(a, u);
             }
             __syncthreads();
