@@ -89,8 +89,13 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
     constexpr bool TW_EARLY = SDDC_TW_EARLY && D <= 1;   // (held to 128 VGPRs by the launch bounds)
     constexpr int NB = N >= 512 ? N / 256 + 1 : 2;
     const int s0 = (tunebin - N / 2) & (HALF - 1), r0 = PRUNE ? s0 >> 8 : 0;
-    // d <= 1: Z is stored rotated by the tune bin, bin j at swz((j - tb) mod 4096), so the
-    // inverse's reads of bins tb + m are sT + 256 r with no wrap (the mirror reads keep theirs).
+    // Z (forward pass 2 -> split) is stored without the XOR swizzle, bin j at j: the split's
+    // reads are runs of consecutive bins, ascending (Z_k) and descending (the mirror), which an
+    // XOR swizzle turns into one 2-way bank conflict per 32-lane group wherever a run crosses a
+    // 16-bin block (32 conflict cycles per wave-frame at d = 0), while the pass-2 writes (16
+    // consecutive bins per instruction) need no swizzle.
+    // d <= 1: Z is stored rotated by the tune bin, bin j at (j - tb) mod 4096, so the
+    // inverse's reads of bins tb + m are t + 256 r with no wrap (the mirror reads keep theirs).
     // Forward pass 2 gets it for free: per-lane twiddle bases rotated by 256 zr make output
     // register r hold bin t + 256 (r + zr), i.e. tb + ((t - tb) mod 256) + 256 r.  d = 0 +1.5-2 %,
     // d = 1 +1 % (profiles/r02/ab/zrot.txt).
@@ -186,14 +191,14 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
         if constexpr (PRUNE) {
 #pragma unroll
             for (int r = 0; r < 16; r++)   // Z, natural order: the band's and the mirror's registers
-                if (r < NB || ((r - mrel) & 15) < NB) w0[sT + NT * ((r + r0) & 15)] = v[r];
+                if (r < NB || ((r - mrel) & 15) < NB) w0[t + NT * ((r + r0) & 15)] = v[r];
         } else if constexpr (ZROT) {
-            const int sZ = swz((t - zd) & 255);
+            const int sZ = (t - zd) & 255;
 #pragma unroll
             for (int r = 0; r < 16; r++) w0[sZ + NT * r] = v[r];   // Z, rotated by tb
         } else {
 #pragma unroll
-            for (int r = 0; r < 16; r++) w0[sT + NT * r] = v[r];   // Z, natural order
+            for (int r = 0; r < 16; r++) w0[t + NT * r] = v[r];   // Z, natural order
         }
         __syncthreads();
 
@@ -203,9 +208,9 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
             float2 u[16];
             {
                 const int b0 = tunebin + t;                  // bin of r = 0
-                const int sb0 = swz(b0);                     // swz(b0 + 256 r - N w) = sb0 + 256 r - N w
+                const int sb0 = b0;
                 // mirror bin, same separability (rotated storage: HALF - b0 - tb)
-                const int sc0 = ZROT ? swz((HALF - b0 - tunebin) & (HALF - 1)) : swz(HALF - b0);
+                const int sc0 = ZROT ? (HALF - b0 - tunebin) & (HALF - 1) : HALF - b0;
                 const char *w0b = reinterpret_cast<const char *>(w0);
                 const unsigned sb0b = 8u * (unsigned)sb0, sc0b = 8u * (unsigned)sc0, tb16 = 16u * (unsigned)t;
                 const __amdgpu_buffer_rsrc_t rpq = buf_rsrc(pqz);
@@ -218,8 +223,8 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
                     // byte offsets: the wrap is one AND, the scale folds away
                     float2 zk;
                     // unpaired (XRD) at d = 1: +1 %; at d = 0 the clobbers cost 5 % (profiles/r02/ab/zrot.txt)
-                    if constexpr (ZROT && D > 0) XRD(zk, w0[sT + (sh & (HALF - 1))]);
-                    else if constexpr (ZROT) zk = w0[sT + (sh & (HALF - 1))];
+                    if constexpr (ZROT && D > 0) XRD(zk, w0[t + (sh & (HALF - 1))]);
+                    else if constexpr (ZROT) zk = w0[t + (sh & (HALF - 1))];
                     else zk = *reinterpret_cast<const float2 *>(w0b + ((sb0b + 8u * (unsigned)sh) & (8u * HALF - 8u)));
                     const float2 zc = *reinterpret_cast<const float2 *>(w0b + ((sc0b - 8u * (unsigned)sh) & (8u * HALF - 8u)));
                     a[r] = split_pq(zk, zc, buf_load16(rpq, tb16, 16u * NT * r));
@@ -285,7 +290,7 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
             if (t < N) {
                 const int m = t;
                 const int bin = tunebin + m - (m >= N / 2 ? N : 0);
-                tv = split_pq(w0[swz(bin & (HALF - 1))], w0[swz((HALF - bin) & (HALF - 1))], pqz[m]);
+                tv = split_pq(w0[bin & (HALF - 1)], w0[(HALF - bin) & (HALF - 1)], pqz[m]);
             }
             __syncthreads();
             if (t < N) w1[swz(t)] = tv;
