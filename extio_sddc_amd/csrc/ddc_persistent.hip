@@ -33,16 +33,10 @@ namespace {
 // (profiles/r02/ab/twrd.txt).
 #define XRD(dst, expr) do { dst = (expr); asm volatile("" ::: "memory"); } while (0)
 
-#ifndef SDDC_ZROT
-#define SDDC_ZROT 1
-#endif
 // Pass-1 table twiddles at d <= 1: issued in two groups (8 + 7) right behind the data reads, so
 // the products wait on two LDS round trips instead of one per ds_read2 pair (the compiler's own
 // schedule); the kernel is held to 128 VGPRs for it.  d = 0 +1-2.7 %, d = 1 +1 %; one group of
 // 15 spills and loses at every d, and at d >= 2 either form loses 1-5 % (profiles/r02/ab/early.txt).
-#ifndef SDDC_TW_EARLY
-#define SDDC_TW_EARLY 1
-#endif
 
 // a[r] *= tbl[(r - 1) S + j] (conjugated for DIR > 0), r = 1..15.  EARLY: the table reads are
 // issued in two groups (8 + 7) right behind the caller's exchange reads, each group before its
@@ -86,7 +80,7 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
     // thread at d >= 4, 6 at d = 3, 10 at d = 2: +5-7 % at d = 3..6, +2-3 % at d = 2
     // (profiles/r02/ab/prune_d3_6.txt, prune_d2.txt).
     constexpr bool PRUNE = N <= 1024;
-    constexpr bool TW_EARLY = SDDC_TW_EARLY && D <= 1;   // (held to 128 VGPRs by the launch bounds)
+    constexpr bool TW_EARLY = D <= 1;   // (held to 128 VGPRs by the launch bounds)
     constexpr int NB = N >= 512 ? N / 256 + 1 : 2;
     const int s0 = (tunebin - N / 2) & (HALF - 1), r0 = PRUNE ? s0 >> 8 : 0;
     // Z (forward pass 2 -> split) is stored without the XOR swizzle, bin j at j: the split's
@@ -99,7 +93,7 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
     // Forward pass 2 gets it for free: per-lane twiddle bases rotated by 256 zr make output
     // register r hold bin t + 256 (r + zr), i.e. tb + ((t - tb) mod 256) + 256 r.  d = 0 +1.5-2 %,
     // d = 1 +1 % (profiles/r02/ab/zrot.txt).
-    constexpr bool ZROT = SDDC_ZROT && !PRUNE;
+    constexpr bool ZROT = !PRUNE;
     const int zd = tunebin & 255;
     const int mrel = ((((1 - s0 - N) & (HALF - 1)) >> 8) - r0) & 15;
     __shared__ __attribute__((aligned(16))) float2 lds[HALF];
@@ -116,8 +110,8 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
 
     // per-thread constants, live for the whole frame loop
     const int zr = ZROT ? (tunebin >> 8) + (tid < zd ? 1 : 0) : r0;
-    const float2 fw1_ = PRUNE || ZROT ? tw4096[(tid + 256 * zr) & (HALF - 1)] : rec_f[tid];
-    const float2 fw4_ = PRUNE || ZROT ? tw4096[(4 * tid + 1024 * zr) & (HALF - 1)] : rec_f[NT + tid];
+    const float2 fw1_ = tw4096[(tid + 256 * zr) & (HALF - 1)];   // rotated bases (PRUNE: r0, ZROT: zr)
+    const float2 fw4_ = tw4096[(4 * tid + 1024 * zr) & (HALF - 1)];
     float2 iw1_ = ZROT ? rec_f[tid] : fw1_, iw4_ = ZROT ? rec_f[NT + tid] : fw4_;
     if constexpr (N >= 512 && N < HALF) {
         if (tid < N / 16) {
@@ -192,13 +186,10 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
 #pragma unroll
             for (int r = 0; r < 16; r++)   // Z, natural order: the band's and the mirror's registers
                 if (r < NB || ((r - mrel) & 15) < NB) w0[t + NT * ((r + r0) & 15)] = v[r];
-        } else if constexpr (ZROT) {
+        } else {
             const int sZ = (t - zd) & 255;
 #pragma unroll
             for (int r = 0; r < 16; r++) w0[sZ + NT * r] = v[r];   // Z, rotated by tb
-        } else {
-#pragma unroll
-            for (int r = 0; r < 16; r++) w0[t + NT * r] = v[r];   // Z, natural order
         }
         __syncthreads();
 
@@ -210,7 +201,7 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
                 const int b0 = tunebin + t;                  // bin of r = 0
                 const int sb0 = b0;
                 // mirror bin, same separability (rotated storage: HALF - b0 - tb)
-                const int sc0 = ZROT ? (HALF - b0 - tunebin) & (HALF - 1) : HALF - b0;
+                const int sc0 = ZROT ? (HALF - b0 - tunebin) & (HALF - 1) : HALF - b0;   // (PRUNE: d = 2, 3)
                 const char *w0b = reinterpret_cast<const char *>(w0);
                 const unsigned sb0b = 8u * (unsigned)sb0, sc0b = 8u * (unsigned)sc0, tb16 = 16u * (unsigned)t;
                 const __amdgpu_buffer_rsrc_t rpq = buf_rsrc(pqz);

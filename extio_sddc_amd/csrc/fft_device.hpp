@@ -106,10 +106,6 @@ __device__ __forceinline__ void dft8(const float2 *v, float2 *o)
     }
 }
 
-#ifndef SDDC_DFT16_FMA
-#define SDDC_DFT16_FMA 1
-#endif
-
 // z (1 + i tau)
 __device__ __forceinline__ float2 rot1(float2 z, float tau)
 {
@@ -134,12 +130,12 @@ __device__ __forceinline__ void ajpm(float2 a, float c, float2 z, float2 &p, flo
 template <int DIR>
 __device__ __forceinline__ void dft16(const float2 *v, float2 *o)
 {
-#if SDDC_DFT16_FMA
     // Second-stage twiddles in tangent form, W^m = cos(m th) (1 + i DIR tan(m th)) with
     // th = 2 pi / 16: each twiddled value enters its radix-4 as a 2-FMA rotation, and the cos
     // scale rides on the FMA that combines it (the pair W^1 / W^3 of columns 1 and 3 shares
-    // one scale through the ratio cos 3th / cos th = tan th).  144 VALU instead of 156, same
-    // results to float rounding.
+    // one scale through the ratio cos 3th / cos th = tan th).  144 VALU instead of 156 for the
+    // plain 4 x 4 form with constant twiddle products (its A/B: profiles/r02/ab/dft16_fma.txt;
+    // the plain form is in git history), same results to float rounding.
     constexpr float kT1 = 0.41421356237309504880f;   // tan(pi/8) = cos(3pi/8) / cos(pi/8)
     constexpr float kT3 = 2.41421356237309504880f;   // tan(3pi/8)
     float2 b[4][4];  // b[n2][k1]
@@ -166,31 +162,10 @@ __device__ __forceinline__ void dft16(const float2 *v, float2 *o)
         axpm(t0, kS16_1, p, o[3], o[11]);
         ajpm<DIR>(t1, kS16_1, q, o[7], o[15]);
     }
-#else
-    float2 b[4][4];  // b[n2][k1]
-#pragma unroll
-    for (int n2 = 0; n2 < 4; n2++)
-        dft4<DIR>(v[n2], v[4 + n2], v[8 + n2], v[12 + n2], b[n2][0], b[n2][1], b[n2][2], b[n2][3]);
-    b[1][1] = tw16<DIR, 1>(b[1][1]);
-    b[1][2] = tw16<DIR, 2>(b[1][2]);
-    b[1][3] = tw16<DIR, 3>(b[1][3]);
-    b[2][1] = tw16<DIR, 2>(b[2][1]);
-    b[2][2] = tw16<DIR, 4>(b[2][2]);
-    b[2][3] = tw16<DIR, 6>(b[2][3]);
-    b[3][1] = tw16<DIR, 3>(b[3][1]);
-    b[3][2] = tw16<DIR, 6>(b[3][2]);
-    b[3][3] = tw16<DIR, 9>(b[3][3]);
-#pragma unroll
-    for (int k1 = 0; k1 < 4; k1++)
-        dft4<DIR>(b[0][k1], b[1][k1], b[2][k1], b[3][k1], o[k1], o[k1 + 4], o[k1 + 8], o[k1 + 12]);
-#endif
 }
 
 // a[r] *= W^{r} for r = 1..15 given the forward-direction W^1 and W^4 of this lane
 // (conjugated for DIR = +1).
-#ifndef SDDC_TWREC_CHEB
-#define SDDC_TWREC_CHEB 1
-#endif
 // p = A w, m = A conj(w) for a unit w
 __device__ __forceinline__ void cmul_pm(float2 A, float2 w, float2 &p, float2 &m)
 {
@@ -210,10 +185,10 @@ __device__ __forceinline__ void twiddle_rec16(float2 *a, float2 w1, float2 w4)
         w1.y = -w1.y;
         w4.y = -w4.y;
     }
-#if SDDC_TWREC_CHEB
     // W^8, W^12 as products; W^{4k +- 1} as pairs A W, A conj(W) sharing the products cos * A
     // (3 ops each); W^2 and W^{4k + 2}, W^15 by one step of the Chebyshev recurrence
-    // W^{m+1} = 2 cos(th) W^m - W^{m-1} (2 FMAs): 38 VALU for the 13 powers instead of 52.
+    // W^{m+1} = 2 cos(th) W^m - W^{m-1} (2 FMAs): 38 VALU for the 13 powers instead of 52 for
+    // all products (that form is in git history; A/B profiles/r02/ab/twrec_hybrid.txt).
     // float32 model over all 4096 bases: worst power error 4.6e-7 (rms 7.1e-8) against 3.2e-7
     // (6.9e-8) for the all-product form; a pure Chebyshev form (28 VALU, 1.3e-6) leaked past the
     // 1e-5 bar on the out-of-band parity case at d = 4 (profiles/r02/ab/cheb.txt).
@@ -240,26 +215,6 @@ __device__ __forceinline__ void twiddle_rec16(float2 *a, float2 w1, float2 w4)
     a[13] = cmul(a[13], w13);
     a[14] = cmul(a[14], w14);
     a[15] = cmul(a[15], w15);
-#else
-    // every power at most three products away
-    const float2 w2 = cmul(w1, w1), w3 = cmul(w2, w1);
-    const float2 w8 = cmul(w4, w4), w12 = cmul(w8, w4);
-    a[1] = cmul(a[1], w1);
-    a[2] = cmul(a[2], w2);
-    a[3] = cmul(a[3], w3);
-    a[4] = cmul(a[4], w4);
-    a[5] = cmul(a[5], cmul(w4, w1));
-    a[6] = cmul(a[6], cmul(w4, w2));
-    a[7] = cmul(a[7], cmul(w4, w3));
-    a[8] = cmul(a[8], w8);
-    a[9] = cmul(a[9], cmul(w8, w1));
-    a[10] = cmul(a[10], cmul(w8, w2));
-    a[11] = cmul(a[11], cmul(w8, w3));
-    a[12] = cmul(a[12], w12);
-    a[13] = cmul(a[13], cmul(w12, w1));
-    a[14] = cmul(a[14], cmul(w12, w2));
-    a[15] = cmul(a[15], cmul(w12, w3));
-#endif
 }
 
 template <int R, int DIR>
