@@ -73,6 +73,12 @@ CASES = [
     (5, 2048, 0, 1, "mix"),
     (6, 1024, 1, 0, "mix"),
     (6, 4, 0, 0, "uniform"),
+    # d <= 1 stores Z rotated by the tune bin (ddc_persistent.hip, ZROT): tune bins just
+    # below / above a 256-bin block boundary, where lanes split between two rotations
+    (0, 1020, 0, 0, "mix"),
+    (0, 3844, 0, 1, "bench"),
+    (1, 260, 1, 0, "uniform"),
+    (1, 2044, 0, 0, "mix"),
     # strong out-of-band tone + weak in-band tone at the BASELINE configs' tune bin (strict bar):
     # C2 (d=0), the C3 decimation sweep (d=1..4) and C4 (d=1, lsb, rand)
     (0, 1024, 0, 0, "oob"),
