@@ -258,6 +258,124 @@ def compute_roofline(workload: str, kern_ms: float):
             "source": v.get("source")}
 
 
+class ChannelRun:
+    """C5 on this rank: channels [lo, hi) of `nch` tune bins 0, 4, ..., 4 (nch - 1) over one shared
+    int16 stream.  N > 1: rank 0 holds the batch and every step sends it to all ranks
+    (shard.broadcast_samples, scatter + all-gather by default), batch i + 1's transfer running
+    while batch i is processed (double-buffered input, shard.pipelined_batches)."""
+
+    def __init__(self, torch, ddc, nch, nblk, d, out_dtype, dev, stream, world, rank, method):
+        from extio_sddc_amd import output_samples
+        from extio_sddc_amd.shard import channel_shard
+        self.torch, self.ddc, self.nblk, self.stream, self.method = torch, ddc, nblk, stream, method
+        self.world, self.dev = world, dev
+        lo, hi = channel_shard(nch, world, rank)
+        self.tbs = [4 * c for c in range(nch)][lo:hi]
+        self.nch_local = len(self.tbs)
+        self.d_in = make_input(torch, nblk, 0x5DDC, dev) if rank == 0 else \
+            torch.empty(HALF + nblk * BLOCK, dtype=torch.int16, device=dev)
+        self.d_out = torch.empty((self.nch_local, output_samples(d, nblk) * 2), dtype=out_dtype, device=dev)
+        self.batches = None
+        if world > 1:
+            from extio_sddc_amd.shard import pipelined_batches
+            self.d_in2 = self.d_in.clone()
+            self.batches = pipelined_batches([self.d_in, self.d_in2], None, src=0, method=method)   # closed after timing
+
+    def step(self):
+        src = next(self.batches) if self.batches is not None else self.d_in
+        self.ddc.process_channels_device(src, self.nblk, self.tbs, self.d_out, self.stream)
+
+    def close(self):
+        if self.batches is not None:
+            self.batches.close()   # waits for the prefetched broadcast on every rank
+            self.batches = None
+
+    def broadcast_and_compute_alone(self, backend: str, reps: int = 10) -> dict:
+        """The collective and the compute, each timed alone between barriers (max over ranks), so
+        the line shows which of the two bounds the pipelined step."""
+        import torch.distributed as dist
+        from extio_sddc_amd.shard import broadcast_samples
+        torch = self.torch
+        res = []
+        for phase in ("broadcast", "compute"):
+            dist.barrier()
+            torch.cuda.synchronize()
+            tb0 = time.perf_counter()
+            for _ in range(reps):
+                if phase == "broadcast":
+                    broadcast_samples(self.d_in, src=0, method=self.method)
+                else:
+                    self.ddc.process_channels_device(self.d_in, self.nblk, self.tbs, self.d_out, self.stream)
+            torch.cuda.synchronize()
+            res.append((time.perf_counter() - tb0) / reps)
+        tt = torch.tensor(res, dtype=torch.float64, device=self.dev if backend == "nccl" else "cpu")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        b_s, c_s = tt.tolist()
+        batch_bytes = self.d_in.numel() * 2
+        return {"method": self.method, "bytes_per_batch": batch_bytes, "ms": b_s * 1e3,
+                "GBps_inbound_per_rank": batch_bytes / b_s / 1e9,
+                "compute_ms_per_rank": c_s * 1e3, "reps": reps,
+                "note": "each timed alone between barriers, max over ranks; the timed steps overlap "
+                        "batch i + 1's broadcast with batch i's compute"}
+
+
+def c5_leg(torch, dist, args, dev, stream, world: int, rank: int, backend: str) -> dict:
+    """Config C5 (BASELINE.json configs[4]) beside the headline: 1024 channels at d = 4 (decim 32)
+    from one stream, channels sharded over the world's ranks (strong scaling: the stream's rate
+    is fixed, each rank computes 1024 / N channels), the int16 batch sent to every rank each step.
+    Warm-up to a time floor the ranks agree on, then --c5-steps batches between barrier +
+    synchronize, max over ranks."""
+    from extio_sddc_amd import R2iq
+    d5, nblk5, steps = 4, args.c5_nblk, args.c5_steps
+    ddc5 = R2iq(gain=1.0, device=dev.index)
+    ddc5.setDecimate(d5)
+    ch = ChannelRun(torch, ddc5, 1024, nblk5, d5, torch.float32, dev, stream, world, rank, args.bcast)
+    tw0 = time.perf_counter()
+    while True:
+        for _ in range(5):
+            ch.step()
+        torch.cuda.synchronize()
+        done = (time.perf_counter() - tw0) >= 0.1
+        if world > 1:
+            flag = torch.tensor([1 if done else 0], dtype=torch.int32, device=dev if backend == "nccl" else "cpu")
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+            done = bool(flag.item())
+        if done:
+            break
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ch.step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    ch.close()
+    info = ch.broadcast_and_compute_alone(backend) if world > 1 else None
+    t = torch.tensor([wall], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall = t.item()
+    ms = wall * 1e3 / steps
+    in_msps = nblk5 * BLOCK * steps / wall / 1e6
+    # per rank: the whole int16 batch in + its channels' CF32 outputs
+    bytes_rank = nblk5 * BLOCK * algorithmic_bytes_per_sample(d5, ch.nch_local, 8)
+    out = {"config": "C5 1024-channel DDC from one stream, channels sharded over the ranks",
+           "d": d5, "decim": 2 << d5, "channels": 1024, "channels_per_rank": ch.nch_local, "n_gpus": world,
+           "blocks_per_batch": nblk5, "steps": steps, "ms_per_step": ms,
+           "input_MSps": in_msps, "channel_MSps": in_msps * 1024,
+           "scaling": "strong (fixed stream, 1024 / N channels per rank)",
+           "roofline_frac_per_rank": bytes_rank / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+           "bytes_per_rank_per_batch": bytes_rank,
+           "broadcast": info or ("none (one rank)" if world == 1 else None)}
+    del ch, ddc5
+    torch.cuda.empty_cache()
+    return out
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -277,6 +395,10 @@ def main() -> None:
     ap.add_argument("--bcast", choices=["sag", "bcast"], default="sag",
                     help="C5 input broadcast for N > 1: scatter + all-gather over all links (sag) or one "
                          "broadcast collective (shard.broadcast_samples)")
+    ap.add_argument("--no-c5", action="store_true",
+                    help="skip the same-run C5 leg (1024 channels at d = 4, sharded over the ranks)")
+    ap.add_argument("--c5-nblk", type=int, default=256, help="C5 leg: blocks of 65536 per batch")
+    ap.add_argument("--c5-steps", type=int, default=20, help="C5 leg: timed batches")
     ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds of CPU-baseline work")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sweep", action="store_true",
@@ -339,28 +461,8 @@ def main() -> None:
         workload = f"single d={d} nblk={nblk}" + (f" fine_tune={args.fine_tune}" if args.fine_tune else "") \
             + (" cs16" if args.cs16 else "")
     else:
-        from extio_sddc_amd.shard import channel_shard
-        tbs_all = [4 * c for c in range(args.channels)]
-        lo, hi = channel_shard(args.channels, world, rank)
-        tbs = tbs_all[lo:hi]
-        nch_local = len(tbs)
-        d_in = make_input(torch, nblk, 0x5DDC, dev) if rank == 0 else \
-            torch.empty(HALF + nblk * BLOCK, dtype=torch.int16, device=dev)
-        per = output_samples(d, nblk) * 2
-        d_out = torch.empty((nch_local, per), dtype=out_dtype, device=dev)
-
-        if world > 1:
-            # the ingest rank's batch reaches every rank by RCCL broadcast over xGMI; batch
-            # i + 1's broadcast runs while batch i is processed (double-buffered input)
-            from extio_sddc_amd.shard import pipelined_batches
-            d_in2 = d_in.clone()
-            batches = pipelined_batches([d_in, d_in2], None, src=0, method=args.bcast)   # unbounded; closed after timing
-
-            def step():
-                ddc.process_channels_device(next(batches), nblk, tbs, d_out, stream)
-        else:
-            def step():
-                ddc.process_channels_device(d_in, nblk, tbs, d_out, stream)
+        ch = ChannelRun(torch, ddc, args.channels, nblk, d, out_dtype, dev, stream, world, rank, args.bcast)
+        d_in, d_out, tbs, nch_local, step = ch.d_in, ch.d_out, ch.tbs, ch.nch_local, ch.step
         samples_per_step_all = nblk * BLOCK          # one shared stream
         workload = f"channels d={d} nblk={nblk} nch={args.channels}" + (" cs16" if args.cs16 else "")
 
@@ -401,8 +503,8 @@ def main() -> None:
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     kern_ms = ev0.elapsed_time(ev1) / args.steps          # per step on the launch stream
-    if args.mode == "channels" and world > 1:
-        batches.close()                                   # waits for the prefetched broadcast
+    if args.mode == "channels":
+        ch.close()                                        # waits for the prefetched broadcast
     t = torch.tensor([wall, kern_ms], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -412,29 +514,15 @@ def main() -> None:
     # line shows which of the two bounds the pipelined step
     bcast_info = None
     if args.mode == "channels" and world > 1:
-        from extio_sddc_amd.shard import broadcast_samples
-        reps = 10
-        res = []
-        for phase in ("broadcast", "compute"):
-            dist.barrier()
-            torch.cuda.synchronize()
-            tb0 = time.perf_counter()
-            for _ in range(reps):
-                if phase == "broadcast":
-                    broadcast_samples(d_in, src=0, method=args.bcast)
-                else:
-                    ddc.process_channels_device(d_in, nblk, tbs, d_out, stream)
-            torch.cuda.synchronize()
-            res.append((time.perf_counter() - tb0) / reps)
-        tt = torch.tensor(res, dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        b_s, c_s = tt.tolist()
-        batch_bytes = d_in.numel() * 2
-        bcast_info = {"method": args.bcast, "bytes_per_batch": batch_bytes, "ms": b_s * 1e3,
-                      "GBps_inbound_per_rank": batch_bytes / b_s / 1e9,
-                      "compute_ms_per_rank": c_s * 1e3, "reps": reps,
-                      "note": "each timed alone between barriers, max over ranks; the timed steps overlap "
-                              "batch i + 1's broadcast with batch i's compute"}
+        bcast_info = ch.broadcast_and_compute_alone(backend)
+
+    # C5 in the same run (BASELINE.json configs[4]): 1024 channels at d = 4
+    # from one shared stream, sharded over the ranks with the int16 batch sent to every rank
+    # (scatter + all-gather), so the driver's 1/2/4/8-GPU runs measure the sharded C5 path too.
+    # Reported beside the headline, which it does not change.
+    c5 = None
+    if args.mode == "single" and not (args.no_c5 or args.cs16 or args.fine_tune):
+        c5 = c5_leg(torch, dist, args, dev, stream, world, rank, backend)
 
     # BASELINE.md §3 / SURVEY §8(d) C3 + C4 in the same run, while the clocks are at their
     # steady state: GPU rate and roofline per config (the headline value stays the d=0 line)
@@ -497,6 +585,8 @@ def main() -> None:
 
     if bcast_info:
         result["broadcast"] = bcast_info
+    if c5:
+        result["c5"] = c5
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         ns = 16
         sample = d_in[: HALF + ns * BLOCK].cpu().numpy()
