@@ -33,6 +33,16 @@ namespace {
 // (profiles/r02/ab/twrd.txt).
 #define XRD(dst, expr) do { dst = (expr); asm volatile("" ::: "memory"); } while (0)
 
+// Order LDS accesses within one wave: the wave's LDS operations execute in order, so a pass
+// whose readers and writers are all lanes of one wave needs program order only (the fences keep
+// the compiler from moving LDS accesses across), not a workgroup barrier.
+__device__ __forceinline__ void wave_lds_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // Pass-1 table twiddles at d <= 1: issued in two groups (8 + 7) right behind the data reads, so
 // the products wait on two LDS round trips instead of one per ds_read2 pair (the compiler's own
 // schedule); the kernel is held to 128 VGPRs for it.  d = 0 +1-2.7 %, d = 1 +1 %; one group of
@@ -101,6 +111,15 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
     constexpr int SQ = N >= 512 ? N / 256 : N / 16;
     __shared__ __attribute__((aligned(16))) float2 twl[15 * 16 + 15 * SQ];
     float2 *const w0 = lds, *const w1 = lds;   // the pass buffers (one 32 KB frame buffer)
+    // d >= 2: the inverse's last passes run on one wave (N/16 <= 64 butterflies), so they are
+    // ordered within that wave (wave_lds_sync) and the other waves go on to the next frame's
+    // pass 0.  N <= 256: the filtered bins go to their own buffer sb (N <= 256 float2, 2 KB),
+    // so the split needs no barrier between its Z reads and its writes.  7 barriers per frame
+    // instead of 10 at d >= 4, 8 at d = 2, 3: d = 4 +1 %, d = 5, 6 +0.5 %, d = 2, 3 neutral,
+    // bit-identical (profiles/r02/ab/winv.txt); LDS at d = 4 38.7 KB, still 4 workgroups per CU.
+    constexpr bool WINV = N <= 1024;
+    constexpr bool SEPB = N <= 256;
+    __shared__ __attribute__((aligned(16))) float2 sb[SEPB ? N : 1];
 
     const int tid = (int)threadIdx.x;
     const int G = (int)gridDim.x, w = (int)blockIdx.x;
@@ -247,7 +266,8 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
                 table_twiddle<+1, TW_EARLY>(a, twl + 15 * 16, R0, t % R0);
                 dft16<+1>(a, u);
             }
-            __syncthreads();
+            if constexpr (WINV) wave_lds_sync();
+            else __syncthreads();
             if (act) {
                 if constexpr (R0 == 16) {
                     const int b1 = (t >> 4) * 256;
@@ -259,7 +279,8 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
                     for (int r = 0; r < 16; r++) w0[swz(base + R0 * r)] = u[r];
                 }
             }
-            __syncthreads();
+            if constexpr (WINV) wave_lds_sync();
+            else __syncthreads();
             // ---- inverse pass 2 (R16, NS = N/16): recurrence twiddles, overlap-discard write ----
             if (act) {
                 float2 a[16];
@@ -283,27 +304,31 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
                 const int bin = tunebin + m - (m >= N / 2 ? N : 0);
                 tv = split_pq(w0[bin & (HALF - 1)], w0[(HALF - bin) & (HALF - 1)], pqz[m]);
             }
-            __syncthreads();
-            if (t < N) w1[swz(t)] = tv;
+            // SEPB: the bins go to sb, and wave 0 alone runs the two passes below on sb
+            float2 *const v0 = SEPB ? sb : w1, *const v1 = SEPB ? sb : w0;
+            if constexpr (!SEPB) __syncthreads();
+            if (t < N) v0[swz(t)] = tv;
             __syncthreads();
             float2 u[16];
             if (t < 16) {
                 float2 a[R0];
 #pragma unroll
-                for (int r = 0; r < R0; r++) a[r] = w1[swz(t + 16 * r)];
+                for (int r = 0; r < R0; r++) a[r] = v0[swz(t + 16 * r)];
                 dft<R0, +1>(a, u);
             }
-            __syncthreads();
+            if constexpr (SEPB) wave_lds_sync();
+            else __syncthreads();
             if (t < 16) {
 #pragma unroll
-                for (int r = 0; r < R0; r++) w0[swz(R0 * t + r)] = u[r];
+                for (int r = 0; r < R0; r++) v1[swz(R0 * t + r)] = u[r];
             }
-            __syncthreads();
+            if constexpr (SEPB) wave_lds_sync();
+            else __syncthreads();
             constexpr int NB = N / 16;   // = R0
             if (t < NB) {
                 float2 a[16];
 #pragma unroll
-                for (int r = 0; r < 16; r++) a[r] = w0[swz(t + NB * r)];
+                for (int r = 0; r < 16; r++) a[r] = v1[swz(t + NB * r)];
 #pragma unroll
                 for (int r = 1; r < 16; r++) a[r] = TW<+1>(a[r], twl[15 * 16 + (r - 1) * NB + t]);
                 dft16<+1>(a, u);
