@@ -399,6 +399,7 @@ def main() -> None:
                     help="skip the same-run C5 leg (1024 channels at d = 4, sharded over the ranks)")
     ap.add_argument("--c5-nblk", type=int, default=256, help="C5 leg: blocks of 65536 per batch")
     ap.add_argument("--c5-steps", type=int, default=20, help="C5 leg: timed batches")
+    ap.add_argument("--c5-timeout", type=float, default=120.0, help="C5 leg watchdog, seconds")
     ap.add_argument("--cpu-budget", type=float, default=10.0, help="seconds of CPU-baseline work")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-sweep", action="store_true",
@@ -516,13 +517,6 @@ def main() -> None:
     if args.mode == "channels" and world > 1:
         bcast_info = ch.broadcast_and_compute_alone(backend)
 
-    # C5 in the same run (SURVEY.md §8(e), BASELINE.json configs[4]): 1024 channels at d = 4
-    # from one shared stream, sharded over the ranks with the int16 batch sent to every rank
-    # (scatter + all-gather), so the driver's 1/2/4/8-GPU runs measure the sharded C5 path too.
-    # Reported beside the headline, which it does not change.
-    c5 = None
-    if args.mode == "single" and not (args.no_c5 or args.cs16 or args.fine_tune):
-        c5 = c5_leg(torch, dist, args, dev, stream, world, rank, backend)
 
     # BASELINE.md §3 / SURVEY §8(d) C3 + C4 in the same run, while the clocks are at their
     # steady state: GPU rate and roofline per config (the headline value stays the d=0 line)
@@ -585,8 +579,6 @@ def main() -> None:
 
     if bcast_info:
         result["broadcast"] = bcast_info
-    if c5:
-        result["c5"] = c5
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         ns = 16
         sample = d_in[: HALF + ns * BLOCK].cpu().numpy()
@@ -623,6 +615,29 @@ def main() -> None:
         result["sweep"] = sweep
     if rank == 0:
         result["host"] = platform.node()
+    # C5 in the same run (SURVEY.md §8(e), BASELINE.json configs[4]): 1024 channels at d = 4
+    # from one shared stream, sharded over the ranks with the int16 batch sent to every rank
+    # (scatter + all-gather), so the driver's 1/2/4/8-GPU runs measure the sharded C5 path too.
+    # Reported beside the headline, which it does not change.  It runs after the headline is
+    # complete, under a watchdog: should its collectives stall, rank 0 still prints the line
+    # (with the C5 error) and every rank exits.
+    if args.mode == "single" and not (args.no_c5 or args.cs16 or args.fine_tune):
+        import threading
+
+        def stalled():
+            if rank == 0:
+                print(json.dumps(dict(result, c5={"error": f"no result within {args.c5_timeout:.0f} s"})),
+                      flush=True)
+            os._exit(0)
+        dog = threading.Timer(args.c5_timeout, stalled)
+        dog.daemon = True
+        dog.start()
+        try:
+            result["c5"] = c5_leg(torch, dist, args, dev, stream, world, rank, backend)
+        except Exception as e:   # the headline stands on its own
+            result["c5"] = {"error": f"{type(e).__name__}: {e}"}
+        dog.cancel()
+    if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
