@@ -43,6 +43,17 @@ __device__ __forceinline__ void wave_lds_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Swizzled row stores.  Element 16 q + (r ^ x) of a frame buffer (x = t & 15, q >= 0) sits at
+// byte (128 q + 8 x) ^ 8 r: the lane's base A = 128 q + 8 x is formed once per frame, and each
+// of the 16 stores costs one v_xor_b32 with an immediate (an extra row offset 128 r rides on the
+// ds_write immediate), instead of the xor, mask, shift and or the compiler emits for the index.
+// d >= 1: d = 1 +0.6 %, d = 4 +2.8 %, bit-identical; d = 0 0.4 % slower, so it keeps the index
+// form (profiles/r02/ab/xst.txt).
+__device__ __forceinline__ void st_row(float2 *buf, unsigned A, int r, int rstride, float2 v)
+{
+    *(reinterpret_cast<float2 *>(reinterpret_cast<char *>(buf) + (A ^ (8u * (unsigned)r))) + rstride * r) = v;
+}
+
 // Pass-1 table twiddles at d <= 1: issued in two groups (8 + 7) right behind the data reads, so
 // the products wait on two LDS round trips instead of one per ds_read2 pair (the compiler's own
 // schedule); the kernel is held to 128 VGPRs for it.  d = 0 +1-2.7 %, d = 1 +1 %; one group of
@@ -91,6 +102,7 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
     // (profiles/r02/ab/prune_d3_6.txt, prune_d2.txt).
     constexpr bool PRUNE = N <= 1024;
     constexpr bool TW_EARLY = D <= 1;   // (held to 128 VGPRs by the launch bounds)
+    constexpr bool XST = D >= 1;        // st_row stores
     constexpr int NB = N >= 512 ? N / 256 + 1 : 2;
     const int s0 = (tunebin - N / 2) & (HALF - 1), r0 = PRUNE ? s0 >> 8 : 0;
     // Z (forward pass 2 -> split) is stored without the XOR swizzle, bin j at j: the split's
@@ -157,6 +169,9 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
         asm volatile("" : "+v"(fw1), "+v"(fw4), "+v"(iw1), "+v"(iw4));
         const int sT = swz(t);            // swz(t + 256 r) = sT + 256 r
         const int x15 = t & 15;
+        // row-store bases (st_row): 16 t + (r ^ x15) and 256 (t >> 4) + 16 r + (r ^ x15)
+        const unsigned xa0 = 128u * (unsigned)t + 8u * (unsigned)x15;
+        const unsigned xa1 = 2048u * (unsigned)(t >> 4) + 8u * (unsigned)x15;
         const int oblk = blk * 8 * N;   // first output slot of the block (batch-relative)
         const int kc = k;
         // ---- forward pass 0 (R16, NS1): convert + DFT16 from registers ----
@@ -175,7 +190,9 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
         }
         __syncthreads();   // the previous frame's last LDS reads are done
 #pragma unroll
-        for (int r = 0; r < 16; r++) w0[16 * t + (r ^ x15)] = v[r];          // swz(16t + r)
+        for (int r = 0; r < 16; r++)   // swz(16t + r)
+            if constexpr (XST) st_row(w0, xa0, r, 0, v[r]);
+            else w0[16 * t + (r ^ x15)] = v[r];
         __syncthreads();
         // ---- forward pass 1 (R16, NS16): table twiddles W_256^{(t%16) r} ----
         {
@@ -189,7 +206,9 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
         {
             const int b1 = (t >> 4) * 256;                                     // swz(b1 + x15 + 16 r)
 #pragma unroll
-            for (int r = 0; r < 16; r++) w1[b1 + 16 * r + (x15 ^ r)] = v[r];
+            for (int r = 0; r < 16; r++)
+                if constexpr (XST) st_row(w1, xa1, r, 16, v[r]);
+                else w1[b1 + 16 * r + (x15 ^ r)] = v[r];
         }
         __syncthreads();
         // ---- forward pass 2 (R16, NS256): recurrence twiddles W_4096^{t r} ----
@@ -245,7 +264,9 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
             __syncthreads();
             if constexpr (R0 == 16) {
 #pragma unroll
-                for (int r = 0; r < 16; r++) w1[16 * t + (r ^ x15)] = u[r];
+                for (int r = 0; r < 16; r++)
+                    if constexpr (XST) st_row(w1, xa0, r, 0, u[r]);
+                    else w1[16 * t + (r ^ x15)] = u[r];
             } else {
 #pragma unroll
                 for (int r = 0; r < R0; r++) w1[swz(R0 * t + r)] = u[r];
@@ -272,7 +293,9 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
                 if constexpr (R0 == 16) {
                     const int b1 = (t >> 4) * 256;
 #pragma unroll
-                    for (int r = 0; r < 16; r++) w0[b1 + 16 * r + (x15 ^ r)] = u[r];
+                    for (int r = 0; r < 16; r++)
+                        if constexpr (XST) st_row(w0, xa1, r, 16, u[r]);
+                        else w0[b1 + 16 * r + (x15 ^ r)] = u[r];
                 } else {
                     const int base = (t / R0) * (16 * R0) + (t % R0);
 #pragma unroll
