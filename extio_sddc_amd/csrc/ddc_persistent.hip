@@ -54,6 +54,19 @@ __device__ __forceinline__ void st_row(float2 *buf, unsigned A, int r, int rstri
     *(reinterpret_cast<float2 *>(reinterpret_cast<char *>(buf) + (A ^ (8u * (unsigned)r))) + rstride * r) = v;
 }
 
+// Swizzled element Lane + R with no carry between the two (disjoint bits): the swizzle is linear
+// over XOR, swz(Lane ^ R) = swz(Lane) ^ swz(R), so with lane8 = 8 swz(Lane) formed once per pass
+// the byte address is lane8 ^ 8 swz(R), one v_xor_b32 with an immediate per access instead of
+// the add, shift, xor-and-mask and scale the index form costs per access.  Used by the inverse
+// passes at d >= 1 (their N/16-strided reads and R0-row stores): static VALU -115..-124 at
+// d = 1..3, -90 at d = 4; d = 1 +3-5 %, d = 2, 3 +4-5 %, d = 4 +3 %, d = 5, 6 +2 %, bit-identical
+// (profiles/r02/ab/lx_xor_linear_addresses.txt).
+__device__ __forceinline__ float2 &lds_x(float2 *buf, unsigned lane8, int R)
+{
+    return *reinterpret_cast<float2 *>(reinterpret_cast<char *>(buf) + (lane8 ^ (8u * (unsigned)swz(R))));
+}
+#define LX(buf, lane, R) lds_x(buf, 8u * (unsigned)swz(lane), R)
+
 // Pass-1 table twiddles at d <= 1: issued in two groups (8 + 7) right behind the data reads, so
 // the products wait on two LDS round trips instead of one per ds_read2 pair (the compiler's own
 // schedule); the kernel is held to 128 VGPRs for it.  d = 0 +1-2.7 %, d = 1 +1 %; one group of
@@ -269,7 +282,7 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
                     else w1[16 * t + (r ^ x15)] = u[r];
             } else {
 #pragma unroll
-                for (int r = 0; r < R0; r++) w1[swz(R0 * t + r)] = u[r];
+                for (int r = 0; r < R0; r++) LX(w1, R0 * t, r) = u[r];
             }
             __syncthreads();
             // ---- inverse pass 1 (R16, NS = R0): table twiddles W_{16 R0}^{(j%R0) r} ----
@@ -282,7 +295,7 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
                     for (int r = 0; r < 16; r++) XRD(a[r], w1[sT + NT * r]);
                 } else {
 #pragma unroll
-                    for (int r = 0; r < 16; r++) a[r] = w1[swz(t + NB * r)];
+                    for (int r = 0; r < 16; r++) a[r] = LX(w1, t, NB * r);
                 }
                 table_twiddle<+1, TW_EARLY>(a, twl + 15 * 16, R0, t % R0);
                 dft16<+1>(a, u);
@@ -299,7 +312,7 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
                 } else {
                     const int base = (t / R0) * (16 * R0) + (t % R0);
 #pragma unroll
-                    for (int r = 0; r < 16; r++) w0[swz(base + R0 * r)] = u[r];
+                    for (int r = 0; r < 16; r++) LX(w0, base, R0 * r) = u[r];
                 }
             }
             if constexpr (WINV) wave_lds_sync();
@@ -312,7 +325,7 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
                     for (int r = 0; r < 16; r++) XRD(a[r], w0[sT + NT * r]);
                 } else {
 #pragma unroll
-                    for (int r = 0; r < 16; r++) a[r] = w0[swz(t + NB * r)];
+                    for (int r = 0; r < 16; r++) a[r] = LX(w0, t, NB * r);
                 }
                     twiddle_rec16<+1>(a, iw1, iw4);
                 dft16<+1>(a, u);
@@ -336,14 +349,14 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
             if (t < 16) {
                 float2 a[R0];
 #pragma unroll
-                for (int r = 0; r < R0; r++) a[r] = v0[swz(t + 16 * r)];
+                for (int r = 0; r < R0; r++) a[r] = LX(v0, t, 16 * r);
                 dft<R0, +1>(a, u);
             }
             if constexpr (SEPB) wave_lds_sync();
             else __syncthreads();
             if (t < 16) {
 #pragma unroll
-                for (int r = 0; r < R0; r++) v1[swz(R0 * t + r)] = u[r];
+                for (int r = 0; r < R0; r++) LX(v1, R0 * t, r) = u[r];
             }
             if constexpr (SEPB) wave_lds_sync();
             else __syncthreads();
@@ -351,7 +364,7 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
             if (t < NB) {
                 float2 a[16];
 #pragma unroll
-                for (int r = 0; r < 16; r++) a[r] = v1[swz(t + NB * r)];
+                for (int r = 0; r < 16; r++) a[r] = LX(v1, t, NB * r);
 #pragma unroll
                 for (int r = 1; r < 16; r++) a[r] = TW<+1>(a[r], twl[15 * 16 + (r - 1) * NB + t]);
                 dft16<+1>(a, u);
