@@ -35,6 +35,16 @@ constexpr int CHUNK = 128;    // channels per work item
 constexpr int ZC_MAX = 1536;  // compact window of split bins per chunk
 
 __device__ __forceinline__ int swz(int e) { return e ^ ((e >> 4) & 15); }
+// Swizzled element Lane + R with no carry between the two (disjoint bits): swz is linear over
+// XOR, swz(Lane ^ R) = swz(Lane) ^ swz(R), so the byte address is 8 swz(Lane) ^ 8 swz(R), one
+// v_xor_b32 with an immediate per access (8 swz(Lane) is formed once) instead of the add, shift,
+// xor-and-mask and scale of the index form (as ddc_persistent.hip's inverse passes).  Here
+// neutral (C5 +-0.1 %, 128 channels +0.3 %), bit-identical (profiles/r02/ab/chlx_*.txt).
+__device__ __forceinline__ float2 &lds_x(float2 *buf, unsigned lane8, int R)
+{
+    return *reinterpret_cast<float2 *>(reinterpret_cast<char *>(buf) + (lane8 ^ (8u * (unsigned)swz(R))));
+}
+#define LX(buf, lane, R) lds_x(buf, 8u * (unsigned)swz(lane), R)
 
 #ifndef SDDC_CH_NT
 #define SDDC_CH_NT 1          // non-temporal IQ stores
@@ -242,7 +252,7 @@ __global__ __launch_bounds__(NT, 2) void r2iq_channels_v2_kernel(
                 float2 u[16];
                 dft16<+1>(a, u);
 #pragma unroll
-                for (int r = 0; r < 16; r++) wg[swz(16 * l + r)] = u[r];
+                for (int r = 0; r < 16; r++) LX(wg, 16 * l, r) = u[r];
             }
             channel_sync();
             // pass B: radix-RB Stockham step (NS = 16), twiddles W_N^{j q} = W_256^{(256/N) j q}
@@ -257,7 +267,7 @@ __global__ __launch_bounds__(NT, 2) void r2iq_channels_v2_kernel(
                     const int j = l + TPC * b;
                     float2 a[RB];
 #pragma unroll
-                    for (int q = 0; q < RB; q++) a[q] = wg[swz(j + 16 * q)];
+                    for (int q = 0; q < RB; q++) a[q] = LX(wg, j, 16 * q);
 #pragma unroll
                     for (int q = 1; q < RB; q++) a[q] = cmulc(a[q], twl[((256 / N) * q - 1) * 16 + j]);
                     dft<RB, +1>(a, y[b]);
@@ -329,7 +339,7 @@ __global__ __launch_bounds__(NT, 2) void r2iq_channels_v2_kernel(
                     const int j = l + TPC * b;          // butterfly 0..15
                     float2 a[RB], y[RB];
 #pragma unroll
-                    for (int q = 0; q < RB; q++) a[q] = wg[swz(j + 16 * q)];
+                    for (int q = 0; q < RB; q++) a[q] = LX(wg, j, 16 * q);
 #pragma unroll
                     for (int q = 1; q < RB; q++) a[q] = cmulc(a[q], twl[((256 / N) * q - 1) * 16 + j]);
                     dft<RB, +1>(a, y);
@@ -521,7 +531,7 @@ __global__ __launch_bounds__(NT, L2X2 ? SDDC_CHP_WAVES : 2) void r2iq_channels_p
                     for (int r = 0; r < 16; r++) sl[16 * t + (r ^ x15)] = u[r];
                 } else {
 #pragma unroll
-                    for (int r = 0; r < R0; r++) sl[swz(R0 * t + r)] = u[r];
+                    for (int r = 0; r < R0; r++) LX(sl, R0 * t, r) = u[r];
                 }
             }
             __syncthreads();
@@ -531,7 +541,7 @@ __global__ __launch_bounds__(NT, L2X2 ? SDDC_CHP_WAVES : 2) void r2iq_channels_p
             {
                 float2 a[16];
 #pragma unroll
-                for (int r = 0; r < 16; r++) a[r] = sl[swz(jb + NB * r)];
+                for (int r = 0; r < 16; r++) a[r] = LX(sl, jb, NB * r);
 #pragma unroll
                 for (int r = 1; r < 16; r++) a[r] = cmulc(a[r], twl[15 * 16 + (r - 1) * R0 + (jb % R0)]);
                 dft16<+1>(a, u);
@@ -540,14 +550,14 @@ __global__ __launch_bounds__(NT, L2X2 ? SDDC_CHP_WAVES : 2) void r2iq_channels_p
             {
                 const int base = (jb / R0) * (16 * R0) + (jb % R0);
 #pragma unroll
-                for (int r = 0; r < 16; r++) sl[swz(base + R0 * r)] = u[r];
+                for (int r = 0; r < 16; r++) LX(sl, base, R0 * r) = u[r];
             }
             __syncthreads();
             // pass 2: radix 16, NS = N/16, recurrence twiddles W_N^{j r}; overlap-discard store
             {
                 float2 a[16];
 #pragma unroll
-                for (int r = 0; r < 16; r++) a[r] = sl[swz(jb + NB * r)];
+                for (int r = 0; r < 16; r++) a[r] = LX(sl, jb, NB * r);
                 twiddle_rec16<+1>(a, iw1, iw4);
                 dft16<+1>(a, u);
             }
