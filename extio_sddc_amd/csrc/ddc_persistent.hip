@@ -47,8 +47,10 @@ __device__ __forceinline__ void wave_lds_sync()
 // byte (128 q + 8 x) ^ 8 r: the lane's base A = 128 q + 8 x is formed once per frame, and each
 // of the 16 stores costs one v_xor_b32 with an immediate (an extra row offset 128 r rides on the
 // ds_write immediate), instead of the xor, mask, shift and or the compiler emits for the index.
-// d >= 1: d = 1 +0.6 %, d = 4 +2.8 %, bit-identical; d = 0 0.4 % slower, so it keeps the index
-// form (profiles/r02/ab/xst.txt).
+// d >= 1: d = 1 +0.6 %, d = 4 +2.8 %, bit-identical (profiles/r02/ab/xst.txt).  At d = 0 all
+// four row stores together were 0.4 % slower; split up, the forward pass-0 rows lose 1.2-1.7 %
+// and the inverse pass-0 rows gain 0-1.3 % (xst_d0_parts.txt, xst_inv0_confirm.txt), so d = 0
+// takes the latter only.
 __device__ __forceinline__ void st_row(float2 *buf, unsigned A, int r, int rstride, float2 v)
 {
     *(reinterpret_cast<float2 *>(reinterpret_cast<char *>(buf) + (A ^ (8u * (unsigned)r))) + rstride * r) = v;
@@ -115,7 +117,10 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
     // (profiles/r02/ab/prune_d3_6.txt, prune_d2.txt).
     constexpr bool PRUNE = N <= 1024;
     constexpr bool TW_EARLY = D <= 1;   // (held to 128 VGPRs by the launch bounds)
-    constexpr bool XST = D >= 1;        // st_row stores
+    // st_row stores: the forward pass-0 rows at d >= 1 only (at d = 0 1.2-1.7 % slower), the
+    // other rows at every d (inverse pass-0 rows at d = 0: +0.9-1.3 % on one box, xst_d0_parts.txt,
+    // neutral on another, xst_inv0_confirm.txt; bit-identical, 15 VALU fewer)
+    constexpr bool XST = D >= 1, XF0 = XST, XI0 = true;
     constexpr int NB = N >= 512 ? N / 256 + 1 : 2;
     const int s0 = (tunebin - N / 2) & (HALF - 1), r0 = PRUNE ? s0 >> 8 : 0;
     // Z (forward pass 2 -> split) is stored without the XOR swizzle, bin j at j: the split's
@@ -204,7 +209,7 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
         __syncthreads();   // the previous frame's last LDS reads are done
 #pragma unroll
         for (int r = 0; r < 16; r++)   // swz(16t + r)
-            if constexpr (XST) st_row(w0, xa0, r, 0, v[r]);
+            if constexpr (XF0) st_row(w0, xa0, r, 0, v[r]);
             else w0[16 * t + (r ^ x15)] = v[r];
         __syncthreads();
         // ---- forward pass 1 (R16, NS16): table twiddles W_256^{(t%16) r} ----
@@ -278,7 +283,7 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
             if constexpr (R0 == 16) {
 #pragma unroll
                 for (int r = 0; r < 16; r++)
-                    if constexpr (XST) st_row(w1, xa0, r, 0, u[r]);
+                    if constexpr (XI0) st_row(w1, xa0, r, 0, u[r]);
                     else w1[16 * t + (r ^ x15)] = u[r];
             } else {
 #pragma unroll
