@@ -136,6 +136,14 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
     constexpr bool ZROT = !PRUNE;
     const int zd = tunebin & 255;
     const int mrel = ((((1 - s0 - N) & (HALF - 1)) >> 8) - r0) & 15;
+    // d >= 5: the pruned pass 2 keeps registers {0, 1, mrel, mrel + 1}, i.e. the DFT-16 output
+    // groups k1 = r & 3 in {0, 1, mrel & 3, (mrel + 1) & 3}; groups 2, 3 are computed only when
+    // the mirror needs them (dft16_groups, uniform flags): d = 5, 6 +1-2.8 % (tb 192 / 1024),
+    // bit-identical, d = 4 unchanged (profiles/r02/ab/grp5_d5_6*.txt).  At
+    // d = 4 the branches raise the kernel to 142 VGPRs (3 waves/SIMD, 9-13 % slower; held to 128
+    // it spills), so d = 4 keeps dft16 (profiles/r02/ab/grp_partial_dft16*.txt).
+    constexpr bool GRP = PRUNE && NB == 2 && D >= 5;
+    const bool need2 = ((mrel & 3) - 1u) <= 1u, need3 = (mrel & 3) >= 2;
     __shared__ __attribute__((aligned(16))) float2 lds[HALF];
     // pass-1 twiddle tables, copied once per workgroup: [15][16] forward, [15][S] inverse
     constexpr int SQ = N >= 512 ? N / 256 : N / 16;
@@ -235,7 +243,8 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
 #pragma unroll
             for (int r = 0; r < 16; r++) XRD(a[r], w1[sT + NT * r]);
             twiddle_rec16<-1>(a, fw1, fw4);
-            dft16<-1>(a, v);
+            if constexpr (GRP) dft16_groups<-1>(a, v, need2, need3);
+            else dft16<-1>(a, v);
         }
         __syncthreads();
         if constexpr (PRUNE) {

@@ -164,6 +164,47 @@ __device__ __forceinline__ void dft16(const float2 *v, float2 *o)
     }
 }
 
+// dft16 computing only the outputs o[k1 + 4 k2] of the groups k1 = 0, 1 and, when the
+// (wave-uniform) flags ask, k1 = 2, 3: the first stage's k1 = 2, 3 outputs and the whole
+// second-stage group are skipped otherwise (same operations as dft16 for what it computes).
+// The other outputs are left unwritten.
+template <int DIR>
+__device__ __forceinline__ void dft16_groups(const float2 *v, float2 *o, bool need2, bool need3)
+{
+    constexpr float kT1 = 0.41421356237309504880f;
+    constexpr float kT3 = 2.41421356237309504880f;
+    float2 b[4][4];  // b[n2][k1]
+#pragma unroll
+    for (int n2 = 0; n2 < 4; n2++) {
+        const float2 t0 = cadd(v[n2], v[8 + n2]), t1 = csub(v[n2], v[8 + n2]);
+        const float2 t2 = cadd(v[4 + n2], v[12 + n2]), t3 = mulj<DIR>(csub(v[4 + n2], v[12 + n2]));
+        b[n2][0] = cadd(t0, t2);
+        b[n2][1] = cadd(t1, t3);
+        if (need2) b[n2][2] = csub(t0, t2);
+        if (need3) b[n2][3] = csub(t1, t3);
+    }
+    dft4<DIR>(b[0][0], b[1][0], b[2][0], b[3][0], o[0], o[4], o[8], o[12]);
+    float2 t0, t1, p, q;
+    {   // k1 = 1 (as dft16)
+        axpm(b[0][1], kR2, rot1(b[2][1], (float)DIR), t0, t1);
+        axpm(rot1(b[1][1], DIR * kT1), kT1, rot1(b[3][1], DIR * kT3), p, q);
+        axpm(t0, kC16_1, p, o[1], o[9]);
+        ajpm<DIR>(t1, kC16_1, q, o[5], o[13]);
+    }
+    if (need2) {   // k1 = 2
+        ajpm<DIR>(b[0][2], 1.f, b[2][2], t0, t1);
+        axpm(rot1(b[1][2], (float)DIR), -1.f, rot1(b[3][2], (float)-DIR), p, q);
+        axpm(t0, kR2, p, o[2], o[10]);
+        ajpm<DIR>(t1, kR2, q, o[6], o[14]);
+    }
+    if (need3) {   // k1 = 3
+        axpm(b[0][3], -kR2, rot1(b[2][3], (float)-DIR), t0, t1);
+        axpm(rot1(b[1][3], DIR * kT3), -kT3, rot1(b[3][3], DIR * kT1), p, q);
+        axpm(t0, kS16_1, p, o[3], o[11]);
+        ajpm<DIR>(t1, kS16_1, q, o[7], o[15]);
+    }
+}
+
 // a[r] *= W^{r} for r = 1..15 given the forward-direction W^1 and W^4 of this lane
 // (conjugated for DIR = +1).
 // p = A w, m = A conj(w) for a unit w
