@@ -206,7 +206,18 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
             float2 a[16];
 #pragma unroll
             for (int r = 0; r < 16; r++)
-                a[r] = make_float2(derand<RAND>((int)(short)(x[r] & 0xffff)), derand<RAND>(x[r] >> 16));
+                if constexpr (RAND) {
+                    // convert_float<rand> on the int16 pair itself: an odd sample is XORed with
+                    // 0xFFFE (fft_mt_r2iq.h:36-51), i.e. word ^ (word & 0x10001) * 0xFFFE; the
+                    // conversion then stays integer-exact, as without RAND (the compiler's int16
+                    // first-stage butterflies apply): -17 VALU, the d = 0 RAND kernels' 2 spills
+                    // gone; with RAND + LSB d = 0 0 to +0.9 %, d = 1 neutral, d = 4 +1.1 %,
+                    // bit-identical (profiles/r02/ab/irand_rand_lsb.txt)
+                    const int w = x[r] ^ (int)(((unsigned)x[r] & 0x10001u) * 0xFFFEu);
+                    a[r] = make_float2((float)(int)(short)(w & 0xffff), (float)(w >> 16));
+                } else {
+                    a[r] = make_float2((float)(int)(short)(x[r] & 0xffff), (float)(x[r] >> 16));
+                }
             if (++k == FRAMES) {
                 k = 0;
                 ++blk;

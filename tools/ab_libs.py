@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--tunebin", type=int, default=1024)
     ap.add_argument("--channels", type=int, default=0, help="time process_channels_device with tune bins 4c")
     ap.add_argument("--variant", type=int, default=0, help="single-channel kernel (sddc_ddc_internal.h)")
+    ap.add_argument("--rand", action="store_true", help="RAND de-randomisation on (config C4)")
+    ap.add_argument("--lsb", action="store_true", help="sideband inversion on (config C4)")
     args = ap.parse_args()
 
     import torch
@@ -44,6 +46,10 @@ def main():
         rc = L.sddc_ddc_create(1.0, 0, ctypes.byref(h))
         assert rc == 0, L.sddc_ddc_last_error()
         L.sddc_ddc_set_tunebin(h, args.tunebin)
+        if args.rand:
+            assert L.sddc_ddc_set_rand(h, 1) == 0
+        if args.lsb:
+            assert L.sddc_ddc_set_sideband(h, 1) == 0
         if args.variant:
             L.sddc_ddc_internal_set_variant.argtypes = [ctypes.c_void_p, ctypes.c_int]
             assert L.sddc_ddc_internal_set_variant(h, args.variant) == 0
