@@ -35,6 +35,19 @@ hipError_t launch_frames_persistent(const KernelTables &t, int d, const int16_t 
                                     const float2 *nco_trig, int device, hipStream_t s);
 hipError_t launch_build_split_filter(const KernelTables &t, int d, int tunebin, float4 *pq, hipStream_t s);
 
+// d = 0 fused-split kernel (ddc_persistent.hip, FS): used when fs_path(d, tunebin) (d = 0, tunebin a
+// multiple of 4, built with SDDC_D0_FS).  Its per-tunebin tables: pqf (4096 float4, the split x
+// filter by bin in lane order) and fsl (3 x 256 float2, the output modulation's lane factors),
+// built by launch_build_fs_tables.
+#ifndef SDDC_D0_FS
+#define SDDC_D0_FS 1
+#endif
+bool fs_path(int d, int tunebin);
+hipError_t launch_build_fs_tables(const KernelTables &t, int tunebin, float4 *pqf, float2 *fsl, hipStream_t s);
+hipError_t launch_frames_fs(const KernelTables &t, const int16_t *d_in, int nblk, void *d_out, const float4 *pqf,
+                            const float2 *fsl, int tunebin, int lsb, int rand, int cs16, float cs16_scale,
+                            const float2 *nco_starts, const float2 *nco_trig, int device, hipStream_t s);
+
 // many-channel v2 (d = 4..6): persistent, forward once per (frame, 128-channel chunk)
 // stride: scalar components (float or int16) per channel row; cs16 as above.  d_windows:
 // per-128-channel-chunk forward-bin windows from channel_windows (device copy), or nullptr.

@@ -399,6 +399,314 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// d = 0, fused split (FS): the forward pass 2, the r2c split x filter and the inverse pass 0 of
+// a frame run in registers, with no LDS exchange between them.
+//
+// Forward pass 2's butterfly on lane l is column c = kFsPerm[l]: it produces Z[c + 256 k],
+// k = 0..15.  The split of bin b needs Z[-b]; for b = c + 256 k that is Z[(256 - c) + 256 (15 - k)],
+// and lane l ^ 1 holds column 256 - c (the permutation pairs the lanes), so the mirror is the
+// partner lane's register 15 - k: a DPP quad_perm [1,0,3,2] operand of the split's FMAs
+// (v_fmac_f32_dpp, no extra instruction).  The self-mirrored columns 0 and 128 (lanes 0, 1 of
+// wave 0) read their own registers instead (a wave-uniform branch, selects in wave 0 only).
+//
+// The inverse then runs on absolute bin indices: inverse pass 0's butterfly c takes the split
+// values of bins c + 256 s, i.e. the lane's own registers.  The tune shift, which the reference
+// applies as an input offset (T[m] = X[tb + m] H[m], impl.hpp:84-96), becomes the output
+// modulation y[n] = e^{-2 pi i tb n / 4096} y'[n] (y' the inverse FFT over bins):
+//   n = t + 256 k:  e^{-2 pi i tb t / 4096} (lane factor g_t, folded into the last pass's
+//   twiddles) x W_16^{(tb mod 16) k} (a quarter turn per output register: tb is a multiple of 4).
+// The (P, Q) table is indexed by bin (zero out of band) and laid out in lane order.
+// Removed per frame: the Z exchange (16 writes, 32 mirror/band reads per thread, 2 barriers) and
+// the band/mirror address arithmetic; 8 barriers per frame instead of 10.
+// tools/fs_model.py models it step by step against the oracle.
+// ---------------------------------------------------------------------------------------------
+
+// lane -> column of forward pass 2: lanes 2p, 2p+1 hold columns c, 256 - c (lanes 0, 1: 0, 128);
+// chosen (tools/fs_perm.py) so that pass 2's reads (swz(c) mod 32 per 32 lanes) and inverse
+// pass 0's row stores (c mod 16 per 16 lanes) are bank-conflict free up to the one 2-way
+// conflict per 16 lanes that the pairing forces (c = -c mod 16 for c = 0, 8 mod 16).
+#include "ddc_fs_perm.h"
+
+__device__ __forceinline__ float dpp_partner(float v)
+{
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, true));
+}
+
+// f += conj(zp) q for the bin pair (k, 15 - k), zp = the partner lane's registers: the DPP
+// operand feeds the FMA directly.  s_nop 1: a DPP read of a VGPR needs two wait states after
+// the VALU write of it (the compiler cannot see into the asm).
+__device__ __forceinline__ void split_dpp2(float2 &fa, float2 &fb, float2 za, float2 zb, float4 qa, float4 qb)
+{
+    asm("s_nop 1\n\t"
+        "v_fmac_f32_dpp %0, %4, %8 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %0, %5, %9 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %1, %4, %9 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %1, -%5, %8 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %2, %6, %10 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %2, %7, %11 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %3, %6, %11 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %3, -%7, %10 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf"
+        : "+v"(fa.x), "+v"(fa.y), "+v"(fb.x), "+v"(fb.y)
+        : "v"(za.x), "v"(za.y), "v"(zb.x), "v"(zb.y), "v"(qa.z), "v"(qa.w), "v"(qb.z), "v"(qb.w));
+}
+
+// Zk P (own registers)
+__device__ __forceinline__ float2 zk_p(float2 zk, float4 c)
+{
+    return make_float2(fmaf(zk.x, c.x, -zk.y * c.y), fmaf(zk.x, c.y, zk.y * c.x));
+}
+__device__ __forceinline__ float2 zc_q(float2 f, float2 zc, float4 c)
+{
+    f.x = fmaf(zc.x, c.z, f.x);
+    f.x = fmaf(zc.y, c.w, f.x);
+    f.y = fmaf(zc.x, c.w, f.y);
+    f.y = fmaf(-zc.y, c.z, f.y);
+    return f;
+}
+
+// v (-i)^s; s is a constant after unrolling (output register r times W_16^{4 QT r} = (-i)^{QT r})
+__device__ __forceinline__ float2 quarter(float2 v, int s)
+{
+    s &= 3;
+    if (s == 0) return v;
+    if (s == 1) return make_float2(v.y, -v.x);
+    if (s == 2) return make_float2(-v.x, -v.y);
+    return make_float2(-v.y, v.x);
+}
+
+template <int QT, bool NCO, bool CS16>
+__device__ __forceinline__ void emit_frame_q(void *__restrict__ out, int fbase, int k, int t, const float2 (&u)[16],
+                                             const OutArgs &oa, const NcoArgs &nco)
+{
+    const __amdgpu_buffer_rsrc_t ro = buf_rsrc(static_cast<char *>(out) + (size_t)fbase * out_bytes<CS16>());
+    const int r0 = k == 0 ? 4 : 0;   // wave-uniform
+#pragma unroll
+    for (int r = 0; r < 12; r++) {
+        if (r < r0) continue;
+        float2 v = flip(quarter(u[r], QT * r), oa.lsbmask);
+        if constexpr (NCO) v = nco_mix(v, nco, fbase + t + NT * r);
+        store_iq<CS16>(v, ro, (unsigned)t, (unsigned)(NT * r), oa);
+    }
+}
+
+template <bool RAND, bool NCO, bool CS16>
+__global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
+    const int *__restrict__ in32, void *__restrict__ out, int nframes,
+    const float2 *__restrict__ tw_p1, const float2 *__restrict__ tw_q1,
+    const float2 *__restrict__ rec_f, const float2 *__restrict__ tw4096,
+    const float4 *__restrict__ pqf, const float2 *__restrict__ fsl, int tunebin, OutArgs oa, NcoArgs nco)
+{
+    __shared__ __attribute__((aligned(16))) float2 lds[HALF];
+    __shared__ __attribute__((aligned(16))) float2 twl[15 * 16 * 2];   // forward / inverse pass-1 tables
+
+    const int tid = (int)threadIdx.x;
+    const int G = (int)gridDim.x, w = (int)blockIdx.x;
+    const int f0 = (int)(((long long)nframes * w) / G);
+    const int f1 = (int)(((long long)nframes * (w + 1)) / G);
+    if (f0 >= f1) return;
+
+    // per-lane constants: the column, and (reloaded every frame from L2, to keep them out of
+    // the registers of the other passes) the twiddle bases of the two NS = 256 passes
+    const int col_ = kFsPerm[tid];
+    for (int i = tid; i < 15 * 16 * 2; i += NT) twl[i] = i < 15 * 16 ? tw_p1[i] : tw_q1[i - 15 * 16];
+    const int qt = (tunebin >> 2) & 3;               // (tb mod 16) / 4: the output quarter turns
+#ifdef SDDC_FS_FAKE_W0   // timing only: wave 0 takes the DPP path too (lanes 0, 1 wrong)
+    const bool w0 = false;
+#else
+    const bool w0 = __builtin_amdgcn_readfirstlane(tid >> 6) == 0;   // the wave holding columns 0, 128
+#endif
+
+    int blk = f0 / FRAMES, k = f0 - blk * FRAMES;
+    int x[16];
+    load_frame(in32, blk, k, x);
+
+    for (int f = f0; f < f1; f++) {
+        int z = 0;
+        asm volatile("" : "+s"(z));
+        const int t = tid + z;
+        const int c = col_ + z;
+        const int sT = swz(t);
+        const int x15 = t & 15;
+        const int oblk = blk * 8 * HALF;
+        const int kc = k;
+        // ---- forward pass 0 (R16, NS1): convert + DFT16 from registers ----
+        float2 v[16];
+        {
+            float2 a[16];
+#pragma unroll
+            for (int r = 0; r < 16; r++)
+                if constexpr (RAND) {
+                    const int wd = x[r] ^ (int)(((unsigned)x[r] & 0x10001u) * 0xFFFEu);   // as r2iq_persistent_kernel
+                    a[r] = make_float2((float)(int)(short)(wd & 0xffff), (float)(wd >> 16));
+                } else {
+                    a[r] = make_float2((float)(int)(short)(x[r] & 0xffff), (float)(x[r] >> 16));
+                }
+            if (++k == FRAMES) {
+                k = 0;
+                ++blk;
+            }
+            if (f + 1 < f1) load_frame(in32, blk, k, x);   // prefetch the next frame
+            dft16<-1>(a, v);
+        }
+        __syncthreads();   // the previous frame's last LDS reads are done
+#pragma unroll
+        for (int r = 0; r < 16; r++) lds[16 * t + (r ^ x15)] = v[r];
+        __syncthreads();
+        // ---- forward pass 1 (R16, NS16): table twiddles W_256^{(t%16) r} ----
+        const float2 fw1 = tw4096[c], fw4 = tw4096[(4 * c) & (HALF - 1)];   // pass 2: W^c, W^{4c}
+        {
+            float2 a[16];
+#pragma unroll
+            for (int r = 0; r < 16; r++) XRD(a[r], lds[sT + NT * r]);
+            table_twiddle<-1, true>(a, twl, 16, x15);
+            dft16<-1>(a, v);
+        }
+        __syncthreads();
+        {
+            const int b1 = (t >> 4) * 256;
+#pragma unroll
+            for (int r = 0; r < 16; r++) lds[b1 + 16 * r + (x15 ^ r)] = v[r];
+        }
+        __syncthreads();
+        // ---- forward pass 2 (R16, NS256) on column c: Z[c + 256 k] in v[k] ----
+        // The split's (P, Q) loads (bin pairs p, 15 - p) run a pair ahead of their use, the first
+        // issued before pass 2 so that its reads and arithmetic cover the L2 latency (an empty asm
+        // with a memory clobber pins each group; the compiler's own schedule waits for every pair
+        // right after issuing it).  Two pairs ahead of pass 2 spill at 128 VGPRs.
+        const __amdgpu_buffer_rsrc_t rpq = buf_rsrc(pqf + z);
+        const unsigned t16 = 16u * (unsigned)t;
+        float4 qa[8], qb[8];
+#pragma unroll
+        for (int p = 0; p < 1; p++) {
+            qa[p] = buf_load16(rpq, t16, 16u * NT * p);
+            qb[p] = buf_load16(rpq, t16, 16u * NT * (15 - p));
+        }
+        asm volatile("" ::: "memory");
+        {
+            float2 a[16];
+            const int sC = swz(c);
+#pragma unroll
+            for (int r = 0; r < 16; r++) XRD(a[r], lds[sC + NT * r]);
+            twiddle_rec16<-1>(a, fw1, fw4);
+            dft16<-1>(a, v);
+        }
+        // ---- split x filter (bins c + 256 k, mirror from the partner lane) -> inverse pass 0 ----
+        float2 u[16];
+        {
+            float2 a[16];
+            if (!w0) {
+#pragma unroll
+                for (int p = 0; p < 8; p++) {
+                    if (p + 1 < 8) {
+                        qa[p + 1] = buf_load16(rpq, t16, 16u * NT * (p + 1));
+                        qb[p + 1] = buf_load16(rpq, t16, 16u * NT * (15 - 1 - p));
+                        asm volatile("" ::: "memory");
+                    }
+                    float2 fa = zk_p(v[p], qa[p]), fb = zk_p(v[15 - p], qb[p]);
+                    split_dpp2(fa, fb, v[15 - p], v[p], qa[p], qb[p]);
+                    a[p] = fa;
+                    a[15 - p] = fb;
+                }
+            } else {
+                // wave 0: lanes 0 (column 0: mirror of register k is its own (16 - k) mod 16) and
+                // 1 (column 128: its own 15 - k) are self-mirrored
+                const int lane = t & 63;
+#pragma unroll
+                for (int p = 0; p < 8; p++) {
+                    if (p + 1 < 8) {
+                        qa[p + 1] = buf_load16(rpq, t16, 16u * NT * (p + 1));
+                        qb[p + 1] = buf_load16(rpq, t16, 16u * NT * (15 - 1 - p));
+                        asm volatile("" ::: "memory");
+                    }
+#pragma unroll
+                    for (int h = 0; h < 2; h++) {
+                        const int kk = h ? 15 - p : p;
+                        const float4 q = h ? qb[p] : qa[p];
+                        const float2 vm = v[15 - kk], v0m = v[(16 - kk) & 15];
+                        float2 zc = make_float2(dpp_partner(vm.x), dpp_partner(vm.y));
+                        zc = lane == 1 ? vm : zc;
+                        zc = lane == 0 ? v0m : zc;
+                        a[kk] = zc_q(zk_p(v[kk], q), zc, q);
+                    }
+                }
+            }
+            dft16<+1>(a, u);
+        }
+        __syncthreads();   // every wave's pass-2 reads are done
+        {
+            const unsigned xc0 = 128u * (unsigned)c + 8u * (unsigned)(c & 15);   // row 16 c + (r ^ (c & 15))
+#pragma unroll
+            for (int r = 0; r < 16; r++) st_row(lds, xc0, r, 0, u[r]);
+        }
+        __syncthreads();
+        // ---- inverse pass 1 (R16, NS16): table twiddles W_256^{-(t%16) r} ----
+        // inverse pass 2's bases: W^t, W^{4t} and the lane's modulation factor g_t
+        const float2 rw1 = rec_f[t], rw4 = rec_f[NT + t], g0 = fsl[t];
+        {
+            float2 a[16];
+#pragma unroll
+            for (int r = 0; r < 16; r++) XRD(a[r], lds[sT + NT * r]);
+            table_twiddle<+1, true>(a, twl + 15 * 16, 16, x15);
+            dft16<+1>(a, u);
+        }
+        __syncthreads();
+        {
+            const int b1 = (t >> 4) * 256;
+#pragma unroll
+            for (int r = 0; r < 16; r++) lds[b1 + 16 * r + (x15 ^ r)] = u[r];
+        }
+        __syncthreads();
+        // ---- inverse pass 2 (R16, NS256): twiddles g_t W^{-t r}, quarter turns, overlap-discard ----
+        {
+            float2 a[16];
+#pragma unroll
+            for (int r = 0; r < 16; r++) XRD(a[r], lds[sT + NT * r]);
+            twiddle_g16<+1>(a, g0, cmulc(g0, rw1), cmulc(g0, rw4), rw1, rw4);   // g W^{-t}, g W^{-4t}
+            dft16<+1>(a, u);
+            const int fb = oblk + emit_base<HALF>(kc);
+            switch (qt) {
+            case 0: emit_frame_q<0, NCO, CS16>(out, fb, kc, t, u, oa, nco); break;
+            case 1: emit_frame_q<1, NCO, CS16>(out, fb, kc, t, u, oa, nco); break;
+            case 2: emit_frame_q<2, NCO, CS16>(out, fb, kc, t, u, oa, nco); break;
+            default: emit_frame_q<3, NCO, CS16>(out, fb, kc, t, u, oa, nco); break;
+            }
+        }
+    }
+}
+
+// FS tables of one tunebin: pqf[l + 256 k] = (P, Q) of bin b = kFsPerm[l] + 256 k (inverse input
+// m = (b - tb) mod 4096, zero unless b is in the reference's band: tb <= b < tb + 2048, b < 4096,
+// or tb - 2048 <= b < tb); fsl = [g_t | g_t W^{-t} | g_t W^{-4t}], g_t = e^{-2 pi i tb t / 4096},
+// looked up exactly in the 4096-point table.
+__global__ void build_fs_tables_kernel(const float2 *__restrict__ hsel0, const float2 *__restrict__ post8192,
+                                       const float2 *__restrict__ tw4096, int tunebin, float4 *__restrict__ pqf,
+                                       float2 *__restrict__ fsl)
+{
+    const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (i >= HALF) return;
+    const int l = i & (NT - 1), kk = i >> 8;
+    const int b = kFsPerm[l] + NT * kk;
+    const bool band = (b >= tunebin && b - tunebin < HALF / 2) || (b < tunebin && tunebin - b <= HALF / 2);
+    float4 c = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (band) {
+        const int m = (b - tunebin) & (HALF - 1);
+        const double hr = hsel0[m].x, hi = hsel0[m].y;
+        const double wr = post8192[b].x, wi = post8192[b].y;
+        const double pr = 1.0 + wi, pi = -wr, qr = 1.0 - wi, qi = wr;   // 1 - i W, 1 + i W
+        c.x = (float)(hr * pr - hi * pi);
+        c.y = (float)(hr * pi + hi * pr);
+        c.z = (float)(hr * qr - hi * qi);
+        c.w = (float)(hr * qi + hi * qr);
+    }
+    pqf[i] = c;
+    if (i < NT) {
+        fsl[i] = tw4096[(tunebin * i) & (HALF - 1)];
+        fsl[NT + i] = tw4096[((tunebin - 1) * i) & (HALF - 1)];
+        fsl[2 * NT + i] = tw4096[((tunebin - 4) * i) & (HALF - 1)];
+    }
+}
+
 // Split x filter coefficients for one (d, tunebin): pq[m] = (P, Q) of inverse input m, with
 // bin = tb + m - (m >= N/2 ? N : 0) (fft_mt_r2iq_impl.hpp:84-98); zero outside [0, 4096).
 // Evaluated in double from the float tables and rounded once.
@@ -461,6 +769,31 @@ hipError_t launch_v(const KernelTables &t, const Launch &L)
     return hipGetLastError();
 }
 
+int g_occupancy_fs[8] = {};
+
+template <bool RAND, bool NCO, bool CS16>
+hipError_t launch_fs_v(const KernelTables &t, const Launch &L, const float4 *pqf, const float2 *fsl)
+{
+    auto kern = r2iq_fs_kernel<RAND, NCO, CS16>;
+    int &occ = g_occupancy_fs[(RAND ? 4 : 0) + (NCO ? 2 : 0) + (CS16 ? 1 : 0)];
+    if (occ == 0) {
+        int nb = 0;
+        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, NT, 0);
+        if (e != hipSuccess) return e;
+        int cus = 0;
+        e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, L.device);
+        if (e != hipSuccess) return e;
+        g_cus = cus;
+        occ = nb > 0 ? nb : 1;
+    }
+    const int nframes = L.nblk * FRAMES;
+    int grid = g_cus * occ;
+    if (grid > nframes) grid = nframes;
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), 0, L.s, reinterpret_cast<const int *>(L.d_in),
+                       L.d_out, nframes, t.tw_p1, t.tw_q1[0], t.rec_f, t.tw4096, pqf, fsl, L.tunebin, L.oa, L.nco);
+    return hipGetLastError();
+}
+
 template <int D, bool RAND, bool NCO>
 hipError_t launch_f(const KernelTables &t, const Launch &L, bool cs16)
 {
@@ -484,6 +817,41 @@ hipError_t launch_build_split_filter(const KernelTables &t, int d, int tunebin, 
     hipLaunchKernelGGL(build_split_filter_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, t.hsel[d],
                        t.post8192, N, tunebin, pq);
     return hipGetLastError();
+}
+
+bool fs_path(int d, int tunebin)
+{
+#if SDDC_D0_FS
+    return d == 0 && (tunebin & 3) == 0;
+#else
+    (void)d;
+    (void)tunebin;
+    return false;
+#endif
+}
+
+hipError_t launch_build_fs_tables(const KernelTables &t, int tunebin, float4 *pqf, float2 *fsl, hipStream_t s)
+{
+    if (tunebin < 0 || tunebin >= HALF || (tunebin & 3)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(build_fs_tables_kernel, dim3(HALF / 256), dim3(256), 0, s, t.hsel[0], t.post8192, t.tw4096,
+                       tunebin, pqf, fsl);
+    return hipGetLastError();
+}
+
+hipError_t launch_frames_fs(const KernelTables &t, const int16_t *d_in, int nblk, void *d_out, const float4 *pqf,
+                            const float2 *fsl, int tunebin, int lsb, int rand, int cs16, float cs16_scale,
+                            const float2 *nco_starts, const float2 *nco_trig, int device, hipStream_t s)
+{
+    if (tunebin & 3) return hipErrorInvalidValue;
+    const Launch L{d_in, nblk, d_out, nullptr, tunebin, device, s, OutArgs{lsb ? 0x80000000u : 0u, cs16_scale},
+                   NcoArgs{nco_starts, nco_trig}};
+    const bool nco = nco_starts != nullptr;
+    if (rand) {
+        if (nco) return cs16 ? launch_fs_v<true, true, true>(t, L, pqf, fsl) : launch_fs_v<true, true, false>(t, L, pqf, fsl);
+        return cs16 ? launch_fs_v<true, false, true>(t, L, pqf, fsl) : launch_fs_v<true, false, false>(t, L, pqf, fsl);
+    }
+    if (nco) return cs16 ? launch_fs_v<false, true, true>(t, L, pqf, fsl) : launch_fs_v<false, true, false>(t, L, pqf, fsl);
+    return cs16 ? launch_fs_v<false, false, true>(t, L, pqf, fsl) : launch_fs_v<false, false, false>(t, L, pqf, fsl);
 }
 
 hipError_t launch_frames_persistent(const KernelTables &t, int d, const int16_t *d_in, int nblk, void *d_out,

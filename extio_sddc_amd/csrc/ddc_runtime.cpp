@@ -204,6 +204,9 @@ struct sddc_ddc {
     // the d = 0 wave kernel's per-tunebin tables: pqW (4096 float4) then twI (4096 float2)
     float4 *d_wave = nullptr;
     int wave_tb = -1;
+    // the d = 0 fused-split kernel's per-tunebin tables: pqf (4096 float4) then fsl (768 float2)
+    float4 *d_fs = nullptr;
+    int fs_tb = -1;
     Readers readers;
 
     // fused fine-tune NCO: host chain + per-launch [T | lane starts] staged through a
@@ -370,6 +373,7 @@ int sddc_ddc_create(float gain, int device, sddc_ddc_t **out)
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipMalloc(&h->d_pq, SDDC_DDC_HALF_FFT * sizeof(float4));
     if (e == hipSuccess) e = hipMalloc(&h->d_wave, 4096 * (sizeof(float4) + sizeof(float2)));
+    if (e == hipSuccess) e = hipMalloc(&h->d_fs, 4096 * sizeof(float4) + 768 * sizeof(float2));
     if (e != hipSuccess) {
         sddc_ddc_destroy(h);
         return fail(SDDC_ERR_HIP, "create: %s", hipGetErrorString(e));
@@ -422,6 +426,7 @@ int sddc_ddc_destroy(sddc_ddc_t *h)
         if (h->d_chscratch) (void)hipFree(h->d_chscratch);
         if (h->d_pq) (void)hipFree(h->d_pq);
         if (h->d_wave) (void)hipFree(h->d_wave);
+        if (h->d_fs) (void)hipFree(h->d_fs);
         (void)h->readers.sync();
         (void)h->ch_readers.sync();
         h->readers.clear();
@@ -590,6 +595,24 @@ static hipError_t launch_single(sddc_ddc_t *h, const int16_t *d_in, int nblk, vo
         if (e != hipSuccess) return e;
         return h->readers.record(s);
     }
+    const float2 *nco_starts = nco ? h->d_nco + sddc::FineTune::kTable : nullptr, *nco_trig = nco ? h->d_nco : nullptr;
+    if (h->variant == 0 && sddc::fs_path(h->d, h->tunebin)) {
+        // d = 0 fused-split kernel: its (P, Q) by bin and output-modulation lane factors
+        float4 *pqf = h->d_fs;
+        float2 *fsl = reinterpret_cast<float2 *>(h->d_fs + 4096);
+        if (h->fs_tb != h->tunebin) {
+            hipError_t e = h->readers.order_before(s);   // launches on other streams may still read them
+            if (e != hipSuccess) return e;
+            e = sddc::launch_build_fs_tables(h->tables, h->tunebin, pqf, fsl, s);
+            if (e != hipSuccess) return e;
+            h->fs_tb = h->tunebin;
+        }
+        hipError_t e = sddc::launch_frames_fs(h->tables, d_in, nblk, d_out, pqf, fsl, h->tunebin, h->lsb, h->rand,
+                                              h->out_fmt == SDDC_DDC_FMT_CS16, h->cs16_scale, nco_starts, nco_trig,
+                                              h->device, s);
+        if (e != hipSuccess) return e;
+        return h->readers.record(s);
+    }
     if (h->pq_d != h->d || h->pq_tb != h->tunebin) {
         hipError_t e = h->readers.order_before(s);   // launches on other streams may still read d_pq
         if (e != hipSuccess) return e;
@@ -598,7 +621,6 @@ static hipError_t launch_single(sddc_ddc_t *h, const int16_t *d_in, int nblk, vo
         h->pq_d = h->d;
         h->pq_tb = h->tunebin;
     }
-    const float2 *nco_starts = nco ? h->d_nco + sddc::FineTune::kTable : nullptr, *nco_trig = nco ? h->d_nco : nullptr;
     hipError_t e = h->d == 0 && h->variant == 7
         ? V->frames_inplace(h->tables, d_in, nblk, d_out, h->d_pq, h->tunebin, h->lsb, h->rand,
                             h->out_fmt == SDDC_DDC_FMT_CS16, h->cs16_scale, nco_starts, nco_trig, h->device, s)

@@ -258,6 +258,43 @@ __device__ __forceinline__ void twiddle_rec16(float2 *a, float2 w1, float2 w4)
     a[15] = cmul(a[15], w15);
 }
 
+// a[r] *= g W^{r} for r = 0..15 (W conjugated for DIR = +1), with g W^0 = u0, g W^1 = u1 and
+// g W^4 = u4 given (exactly rounded, from the table) and the lane's forward W^1, W^4 for the
+// steps: the same products and Chebyshev steps as twiddle_rec16 on the sequence g W^r (the
+// three-term recurrence holds for any geometric sequence), plus the product for r = 0.
+template <int DIR>
+__device__ __forceinline__ void twiddle_g16(float2 *a, float2 u0, float2 u1, float2 u4, float2 w1, float2 w4)
+{
+    if (DIR > 0) {
+        w1.y = -w1.y;
+        w4.y = -w4.y;
+    }
+    const float c1 = w1.x + w1.x;
+    const float2 u8 = cmul(u4, w4), u12 = cmul(u8, w4);
+    float2 u3, u5, u7, u9, u11, u13;
+    cmul_pm(u4, w1, u5, u3);
+    cmul_pm(u8, w1, u9, u7);
+    cmul_pm(u12, w1, u13, u11);
+    const float2 u2 = cheb(c1, u1, u0), u6 = cheb(c1, u5, u4);
+    const float2 u10 = cheb(c1, u9, u8), u14 = cheb(c1, u13, u12), u15 = cheb(c1, u14, u13);
+    a[0] = cmul(a[0], u0);
+    a[1] = cmul(a[1], u1);
+    a[2] = cmul(a[2], u2);
+    a[3] = cmul(a[3], u3);
+    a[4] = cmul(a[4], u4);
+    a[5] = cmul(a[5], u5);
+    a[6] = cmul(a[6], u6);
+    a[7] = cmul(a[7], u7);
+    a[8] = cmul(a[8], u8);
+    a[9] = cmul(a[9], u9);
+    a[10] = cmul(a[10], u10);
+    a[11] = cmul(a[11], u11);
+    a[12] = cmul(a[12], u12);
+    a[13] = cmul(a[13], u13);
+    a[14] = cmul(a[14], u14);
+    a[15] = cmul(a[15], u15);
+}
+
 template <int R, int DIR>
 __device__ __forceinline__ void dft(const float2 *v, float2 *o)
 {
