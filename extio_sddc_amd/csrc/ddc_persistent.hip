@@ -490,6 +490,69 @@ __device__ __forceinline__ void emit_frame_q(void *__restrict__ out, int fbase, 
     }
 }
 
+
+// Diagnostic build (-DSDDC_STAMPS, tools/fs_stamps.py; never the product): per wave, the cycles
+// (s_memtime) of each work segment between two barriers and of each barrier wait, summed over
+// the workgroup's frames in SGPRs, and written once at the end by lane 0 (vector stores) to a
+// stamp buffer of their own: [workgroup][wave][kFsStampWords].  A stamp sits right before and
+// right after each s_barrier, where the barrier's own lgkmcnt(0) drain already is.
+#ifndef SDDC_FS_PQ
+#define SDDC_FS_PQ 1   // (P, Q) bin pairs the FS kernel's split loads run ahead of their use
+#endif
+#ifndef SDDC_FS_PF
+#define SDDC_FS_PF 1   // where the FS kernel issues the next frame's input loads: 0 pass 0, 1 inverse pass 1
+#endif
+constexpr int kFsSegs = 9;                         // work segments: 8 barriers + the frame tail
+constexpr int kFsStampWords = 2 * kFsSegs + 4;     // work[9], wait[9] (wait[8] unused), frames, ticks, rt lo/hi
+#ifdef SDDC_STAMPS
+// SDDC_STAMPS = 1 stamps barriers 0..3, = 2 barriers 4..7 (all eight in one build spill: the
+// accumulators live in SGPRs); the time of an unstamped barrier falls into the next work segment.
+__device__ unsigned g_fs_stamps[2048 * 4 * kFsStampWords];
+constexpr int kStLo = SDDC_STAMPS == 2 ? 4 : 0;
+#define FS_STAMP_INIT()                                                                              \
+    unsigned st_work[kFsSegs] = {}, st_wait[kFsSegs] = {};                                         \
+    unsigned long long st_t = __builtin_amdgcn_s_memtime(), st_a = st_t;                          \
+    const unsigned long long st_t0 = st_t, st_r0 = __builtin_amdgcn_s_memrealtime()
+#define FS_SYNC(i)                                                                                   \
+    do {                                                                                             \
+        if constexpr ((i) >= kStLo && (i) < kStLo + 4) {                                             \
+            st_a = __builtin_amdgcn_s_memtime();                                                     \
+            st_work[i] += (unsigned)(st_a - st_t);                                                   \
+            __syncthreads();                                                                         \
+            st_t = __builtin_amdgcn_s_memtime();                                                     \
+            st_wait[i] += (unsigned)(st_t - st_a);                                                   \
+        } else {                                                                                     \
+            __syncthreads();                                                                         \
+        }                                                                                            \
+    } while (0)
+#define FS_STAMP_FRAME_END()                                                                         \
+    do {                                                                                             \
+        st_a = __builtin_amdgcn_s_memtime();                                                         \
+        st_work[kFsSegs - 1] += (unsigned)(st_a - st_t);                                             \
+        st_t = st_a;                                                                                 \
+    } while (0)
+#define FS_STAMP_WRITE(wg, tid, nfr)                                                                 \
+    do {                                                                                             \
+        const unsigned long long st_r1 = __builtin_amdgcn_s_memrealtime();                          \
+        if (((tid) & 63) == 0) {                                                                     \
+            unsigned *o = g_fs_stamps + ((size_t)(wg) * 4 + ((tid) >> 6)) * kFsStampWords;           \
+            for (int i = 0; i < kFsSegs; i++) {                                                      \
+                o[i] = st_work[i];                                                                   \
+                o[kFsSegs + i] = st_wait[i];                                                         \
+            }                                                                                        \
+            o[2 * kFsSegs] = (unsigned)(nfr);                                                        \
+            o[2 * kFsSegs + 1] = (unsigned)(st_t - st_t0);                                           \
+            o[2 * kFsSegs + 2] = (unsigned)(st_r1 - st_r0);                                          \
+            o[2 * kFsSegs + 3] = (unsigned)SDDC_STAMPS;                                              \
+        }                                                                                            \
+    } while (0)
+#else
+#define FS_STAMP_INIT() (void)0
+#define FS_SYNC(i) __syncthreads()
+#define FS_STAMP_FRAME_END() (void)0
+#define FS_STAMP_WRITE(wg, tid, nfr) (void)0
+#endif
+
 template <bool RAND, bool NCO, bool CS16>
 __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
     const int *__restrict__ in32, void *__restrict__ out, int nframes,
@@ -498,7 +561,14 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
     const float4 *__restrict__ pqf, const float2 *__restrict__ fsl, int tunebin, OutArgs oa, NcoArgs nco)
 {
     __shared__ __attribute__((aligned(16))) float2 lds[HALF];
-    __shared__ __attribute__((aligned(16))) float2 twl[15 * 16 * 2];   // forward / inverse pass-1 tables
+    // pass-1 twiddles W_256^{s r} [15][16] (the inverse pass conjugates them: at d = 0 its table is
+    // the same); the NS = 256 passes' bases W^j, W^{4j} (j < 256: forward pass 2 reads them at the
+    // lane's column, inverse pass 2 at its thread index) and the lane factors g_t.  40832 B per
+    // workgroup: 4 workgroups per CU fill the 160 KB exactly.  In LDS, not registers or L2: the
+    // L2 loads' waits (vmcnt, in issue order) also waited for the input prefetch and the stores.
+    __shared__ __attribute__((aligned(16))) float2 twl[15 * 16];
+    __shared__ __attribute__((aligned(16))) float2 wtab[2 * NT];
+    __shared__ __attribute__((aligned(16))) float2 gtab[NT];
 
     const int tid = (int)threadIdx.x;
     const int G = (int)gridDim.x, w = (int)blockIdx.x;
@@ -509,7 +579,10 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
     // per-lane constants: the column, and (reloaded every frame from L2, to keep them out of
     // the registers of the other passes) the twiddle bases of the two NS = 256 passes
     const int col_ = kFsPerm[tid];
-    for (int i = tid; i < 15 * 16 * 2; i += NT) twl[i] = i < 15 * 16 ? tw_p1[i] : tw_q1[i - 15 * 16];
+    for (int i = tid; i < 15 * 16; i += NT) twl[i] = tw_p1[i];
+    wtab[tid] = rec_f[tid];
+    wtab[NT + tid] = rec_f[NT + tid];
+    gtab[tid] = fsl[tid];
     const int qt = (tunebin >> 2) & 3;               // (tb mod 16) / 4: the output quarter turns
 #ifdef SDDC_FS_FAKE_W0   // timing only: wave 0 takes the DPP path too (lanes 0, 1 wrong)
     const bool w0 = false;
@@ -520,6 +593,7 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
     int blk = f0 / FRAMES, k = f0 - blk * FRAMES;
     int x[16];
     load_frame(in32, blk, k, x);
+    FS_STAMP_INIT();
 
     for (int f = f0; f < f1; f++) {
         int z = 0;
@@ -546,15 +620,16 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
                 k = 0;
                 ++blk;
             }
+#if SDDC_FS_PF == 0
             if (f + 1 < f1) load_frame(in32, blk, k, x);   // prefetch the next frame
+#endif
             dft16<-1>(a, v);
         }
-        __syncthreads();   // the previous frame's last LDS reads are done
+        FS_SYNC(0);   // the previous frame's last LDS reads are done
 #pragma unroll
         for (int r = 0; r < 16; r++) lds[16 * t + (r ^ x15)] = v[r];
-        __syncthreads();
+        FS_SYNC(1);
         // ---- forward pass 1 (R16, NS16): table twiddles W_256^{(t%16) r} ----
-        const float2 fw1 = tw4096[c], fw4 = tw4096[(4 * c) & (HALF - 1)];   // pass 2: W^c, W^{4c}
         {
             float2 a[16];
 #pragma unroll
@@ -562,13 +637,13 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
             table_twiddle<-1, true>(a, twl, 16, x15);
             dft16<-1>(a, v);
         }
-        __syncthreads();
+        FS_SYNC(2);
         {
             const int b1 = (t >> 4) * 256;
 #pragma unroll
             for (int r = 0; r < 16; r++) lds[b1 + 16 * r + (x15 ^ r)] = v[r];
         }
-        __syncthreads();
+        FS_SYNC(3);
         // ---- forward pass 2 (R16, NS256) on column c: Z[c + 256 k] in v[k] ----
         // The split's (P, Q) loads (bin pairs p, 15 - p) run a pair ahead of their use, the first
         // issued before pass 2 so that its reads and arithmetic cover the L2 latency (an empty asm
@@ -578,7 +653,7 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
         const unsigned t16 = 16u * (unsigned)t;
         float4 qa[8], qb[8];
 #pragma unroll
-        for (int p = 0; p < 1; p++) {
+        for (int p = 0; p < SDDC_FS_PQ; p++) {
             qa[p] = buf_load16(rpq, t16, 16u * NT * p);
             qb[p] = buf_load16(rpq, t16, 16u * NT * (15 - p));
         }
@@ -588,9 +663,13 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
             const int sC = swz(c);
 #pragma unroll
             for (int r = 0; r < 16; r++) XRD(a[r], lds[sC + NT * r]);
+            const float2 fw1 = wtab[c], fw4 = wtab[NT + c];   // W^c, W^{4c}
             twiddle_rec16<-1>(a, fw1, fw4);
             dft16<-1>(a, v);
         }
+#if SDDC_FS_PF == 3
+        if (f + 1 < f1) load_frame(in32, blk, k, x);   // the next frame's input
+#endif
         // ---- split x filter (bins c + 256 k, mirror from the partner lane) -> inverse pass 0 ----
         float2 u[16];
         {
@@ -598,9 +677,9 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
             if (!w0) {
 #pragma unroll
                 for (int p = 0; p < 8; p++) {
-                    if (p + 1 < 8) {
-                        qa[p + 1] = buf_load16(rpq, t16, 16u * NT * (p + 1));
-                        qb[p + 1] = buf_load16(rpq, t16, 16u * NT * (15 - 1 - p));
+                    if (p + SDDC_FS_PQ < 8) {
+                        qa[p + SDDC_FS_PQ] = buf_load16(rpq, t16, 16u * NT * (p + SDDC_FS_PQ));
+                        qb[p + SDDC_FS_PQ] = buf_load16(rpq, t16, 16u * NT * (15 - SDDC_FS_PQ - p));
                         asm volatile("" ::: "memory");
                     }
                     float2 fa = zk_p(v[p], qa[p]), fb = zk_p(v[15 - p], qb[p]);
@@ -614,9 +693,9 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
                 const int lane = t & 63;
 #pragma unroll
                 for (int p = 0; p < 8; p++) {
-                    if (p + 1 < 8) {
-                        qa[p + 1] = buf_load16(rpq, t16, 16u * NT * (p + 1));
-                        qb[p + 1] = buf_load16(rpq, t16, 16u * NT * (15 - 1 - p));
+                    if (p + SDDC_FS_PQ < 8) {
+                        qa[p + SDDC_FS_PQ] = buf_load16(rpq, t16, 16u * NT * (p + SDDC_FS_PQ));
+                        qb[p + SDDC_FS_PQ] = buf_load16(rpq, t16, 16u * NT * (15 - SDDC_FS_PQ - p));
                         asm volatile("" ::: "memory");
                     }
 #pragma unroll
@@ -633,35 +712,47 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
             }
             dft16<+1>(a, u);
         }
-        __syncthreads();   // every wave's pass-2 reads are done
+        FS_SYNC(4);   // every wave's pass-2 reads are done
         {
             const unsigned xc0 = 128u * (unsigned)c + 8u * (unsigned)(c & 15);   // row 16 c + (r ^ (c & 15))
 #pragma unroll
             for (int r = 0; r < 16; r++) st_row(lds, xc0, r, 0, u[r]);
         }
-        __syncthreads();
+        FS_SYNC(5);
+#if SDDC_FS_PF == 1
+        // the next frame's input: issued here rather than in pass 0, so its 16 registers are
+        // free through forward pass 2 and the split, and the loads' waits never hold pass 2
+        if (f + 1 < f1) load_frame(in32, blk, k, x);
+#endif
         // ---- inverse pass 1 (R16, NS16): table twiddles W_256^{-(t%16) r} ----
         // inverse pass 2's bases: W^t, W^{4t} and the lane's modulation factor g_t
-        const float2 rw1 = rec_f[t], rw4 = rec_f[NT + t], g0 = fsl[t];
         {
             float2 a[16];
 #pragma unroll
             for (int r = 0; r < 16; r++) XRD(a[r], lds[sT + NT * r]);
-            table_twiddle<+1, true>(a, twl + 15 * 16, 16, x15);
+            table_twiddle<+1, true>(a, twl, 16, x15);
             dft16<+1>(a, u);
         }
-        __syncthreads();
+        FS_SYNC(6);
         {
-            const int b1 = (t >> 4) * 256;
+            // the same addresses as the forward pass-1 stores: recomputed from an opaque copy of
+            // t, or the compiler keeps those 16 addresses live through pass 2 and spills them
+            int t1 = t;
+            asm volatile("" : "+v"(t1));
+            const int b1 = (t1 >> 4) * 256, y15 = t1 & 15;
 #pragma unroll
-            for (int r = 0; r < 16; r++) lds[b1 + 16 * r + (x15 ^ r)] = u[r];
+            for (int r = 0; r < 16; r++) lds[b1 + 16 * r + (y15 ^ r)] = u[r];
         }
-        __syncthreads();
+        FS_SYNC(7);
+#if SDDC_FS_PF == 2
+        if (f + 1 < f1) load_frame(in32, blk, k, x);   // the next frame's input
+#endif
         // ---- inverse pass 2 (R16, NS256): twiddles g_t W^{-t r}, quarter turns, overlap-discard ----
         {
             float2 a[16];
 #pragma unroll
             for (int r = 0; r < 16; r++) XRD(a[r], lds[sT + NT * r]);
+            const float2 rw1 = wtab[t], rw4 = wtab[NT + t], g0 = gtab[t];   // W^t, W^{4t}, g_t
             twiddle_g16<+1>(a, g0, cmulc(g0, rw1), cmulc(g0, rw4), rw1, rw4);   // g W^{-t}, g W^{-4t}
             dft16<+1>(a, u);
             const int fb = oblk + emit_base<HALF>(kc);
@@ -672,7 +763,9 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
             default: emit_frame_q<3, NCO, CS16>(out, fb, kc, t, u, oa, nco); break;
             }
         }
+        FS_STAMP_FRAME_END();
     }
+    FS_STAMP_WRITE(w, tid, f1 - f0);
 }
 
 // FS tables of one tunebin: pqf[l + 256 k] = (P, Q) of bin b = kFsPerm[l] + 256 k (inverse input
@@ -874,3 +967,20 @@ hipError_t launch_frames_persistent(const KernelTables &t, int d, const int16_t 
 }
 
 }  // namespace sddc
+
+// Diagnostic (SDDC_STAMPS builds only): copy the d = 0 fused-split kernel's stamp buffer of the
+// last launch ([workgroup][wave][words], tools/fs_stamps.py) to host memory; -1 in product builds.
+extern "C" int sddc_ddc_internal_fs_stamps(unsigned *host, int nwords, int *words_per_wave)
+{
+    if (words_per_wave) *words_per_wave = sddc::kFsStampWords;
+#ifdef SDDC_STAMPS
+    const size_t n = sizeof(sddc::g_fs_stamps) / sizeof(unsigned);
+    if (!host || nwords < 0 || (size_t)nwords > n) return -2;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(sddc::g_fs_stamps), (size_t)nwords * sizeof(unsigned), 0,
+                               hipMemcpyDeviceToHost) == hipSuccess ? 0 : -3;
+#else
+    (void)host;
+    (void)nwords;
+    return -1;
+#endif
+}
