@@ -149,13 +149,36 @@ print(done, time.perf_counter() - t0)
 """
 
 
-def _distinct_core_cpus(limit: int):
-    """CPUs of this process's affinity set, at most one per physical core (SMT siblings
-    skipped), at most `limit` (the GPU box's CPU share is 16)."""
+def _cgroup_cpu_quota():
+    """CPUs this process may keep busy by its cgroup (v2 cpu.max, v1 cfs quota), or None if unlimited."""
+    for path, parse in (("/sys/fs/cgroup/cpu.max", lambda t: t.split()),
+                        ("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", None)):
+        try:
+            with open(path) as f:
+                txt = f.read().strip()
+        except OSError:
+            continue
+        if parse:
+            q, per = parse(txt)
+            if q == "max":
+                return None
+            return max(1, int(int(q) // int(per)))
+        q = int(txt)
+        if q <= 0:
+            return None
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            return max(1, q // int(f.read().strip()))
+    return None
+
+
+def _distinct_core_cpus():
+    """CPUs of this process's affinity set, one per physical core (SMT siblings skipped), capped
+    by the cgroup CPU quota when one is set: (cpus, affinity size, quota or None)."""
     try:
         aff = sorted(os.sched_getaffinity(0))
     except AttributeError:
         aff = list(range(os.cpu_count() or 1))
+    quota = _cgroup_cpu_quota()
     picked, seen = [], set()
     for c in aff:
         try:
@@ -170,18 +193,18 @@ def _distinct_core_cpus(limit: int):
             continue
         seen.add(key)
         picked.append(c)
-        if len(picked) >= limit:
-            break
-    return picked, len(aff)
+    if quota is not None:
+        picked = picked[:quota]
+    return picked, len(aff), quota
 
 
 def cpu_baseline_all_cores(d: int, tunebin: int, sample_in: np.ndarray, nblk_sample: int, budget_s: float) -> dict:
     """one independent CPU-backend instance per physical core of this
-    process's CPU share (at most 16, the GPU box's share), each a child process pinned to its own
-    core that never touches the GPU; aggregate input MS/s."""
+    process's affinity set (capped by the cgroup CPU quota, which the line states), each a child
+    process pinned to its own core that never touches the GPU; aggregate input MS/s."""
     import tempfile
     from extio_sddc_amd._lib import LIB_PATH
-    cpus, naff = _distinct_core_cpus(16)
+    cpus, naff, quota = _distinct_core_cpus()
     with tempfile.TemporaryDirectory(dir="/tmp") as td:
         path = os.path.join(td, "sample.npy")
         np.save(path, sample_in)
@@ -195,7 +218,9 @@ def cpu_baseline_all_cores(d: int, tunebin: int, sample_in: np.ndarray, nblk_sam
             done, dt = out.split()
             total += int(done) * BLOCK / float(dt)
     return {"value": total / 1e6, "unit": "input MSamples/s", "cores": len(cpus), "kind": "port",
-            "cpus": cpus, "affinity_cpus": naff,
+            "cpus": cpus, "affinity_cpus": naff, "cgroup_cpu_quota": quota,
+            "core_budget": ("every physical core of the affinity set" if quota is None else
+                            f"the cgroup CPU quota ({quota} CPUs), one per physical core"),
             "sample": f"{len(cpus)} independent CPU-backend processes, one per physical core (pinned), "
                       f"x the 1-core sample, {budget_s:.1f} s each"}
 
@@ -276,10 +301,39 @@ class ChannelRun:
             torch.empty(HALF + nblk * BLOCK, dtype=torch.int16, device=dev)
         self.d_out = torch.empty((self.nch_local, output_samples(d, nblk) * 2), dtype=out_dtype, device=dev)
         self.batches = None
+        self.bcast_check = None
         if world > 1:
+            self.bcast_check = self.check_broadcast()
             from extio_sddc_amd.shard import pipelined_batches
             self.d_in2 = self.d_in.clone()
             self.batches = pipelined_batches([self.d_in, self.d_in2], None, src=0, method=method)   # closed after timing
+
+    def check_broadcast(self) -> dict:
+        """One broadcast of the real batch with the chosen method, then the batch's checksum on
+        every rank against rank 0's (int64 sum of the int32 view and of its squares' low bits):
+        a method that delivers wrong bytes on this backend falls back to the plain broadcast."""
+        import torch.distributed as dist
+        from extio_sddc_amd.shard import broadcast_samples
+        torch = self.torch
+
+        def checksum():
+            v = self.d_in.view(torch.int32).to(torch.int64)
+            return torch.stack([v.sum(), (v * v).remainder(1 << 31).sum()])
+        ref = checksum() if dist.get_rank() == 0 else torch.zeros(2, dtype=torch.int64, device=self.d_in.device)
+        broadcast_samples(self.d_in, src=0, method=self.method)
+        got = checksum()
+        dev = self.d_in.device if dist.get_backend() == "nccl" else "cpu"
+        ref = ref.to(dev)
+        dist.broadcast(ref, src=0)
+        bad = torch.tensor([0 if torch.equal(got.to(dev), ref) else 1], dtype=torch.int32, device=dev)
+        dist.all_reduce(bad, op=dist.ReduceOp.MAX)
+        ok = bad.item() == 0
+        out = {"method": self.method, "checksum_equal_on_all_ranks": ok}
+        if not ok and self.method != "bcast":
+            self.method = "bcast"
+            broadcast_samples(self.d_in, src=0, method="bcast")
+            out["fallback"] = "bcast"
+        return out
 
     def step(self):
         src = next(self.batches) if self.batches is not None else self.d_in
@@ -370,7 +424,8 @@ def c5_leg(torch, dist, args, dev, stream, world: int, rank: int, backend: str) 
            "scaling": "strong (fixed stream, 1024 / N channels per rank)",
            "roofline_frac_per_rank": bytes_rank / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
            "bytes_per_rank_per_batch": bytes_rank,
-           "broadcast": info or ("none (one rank)" if world == 1 else None)}
+           "broadcast": info or ("none (one rank)" if world == 1 else None),
+           "broadcast_check": ch.bcast_check}
     del ch, ddc5
     torch.cuda.empty_cache()
     return out
@@ -579,6 +634,8 @@ def main() -> None:
 
     if bcast_info:
         result["broadcast"] = bcast_info
+    if args.mode == "channels" and world > 1:
+        result["broadcast_check"] = ch.bcast_check
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         ns = 16
         sample = d_in[: HALF + ns * BLOCK].cpu().numpy()
@@ -625,10 +682,14 @@ def main() -> None:
         import threading
 
         def stalled():
+            # the headline stands; the stall is reported and the process exits non-zero (3) so the
+            # driver and torchrun see the C5 leg's collective hang
             if rank == 0:
-                print(json.dumps(dict(result, c5={"error": f"no result within {args.c5_timeout:.0f} s"})),
-                      flush=True)
-            os._exit(0)
+                print(json.dumps(dict(result, c5={"error": f"stalled: no result within {args.c5_timeout:.0f} s",
+                                                  "exit_code": 3})), flush=True)
+            print(f"bench.py rank {rank}: C5 leg stalled after {args.c5_timeout:.0f} s, exiting 3",
+                  file=sys.stderr, flush=True)
+            os._exit(3)
         dog = threading.Timer(args.c5_timeout, stalled)
         dog.daemon = True
         dog.start()

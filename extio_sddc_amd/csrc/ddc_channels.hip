@@ -578,10 +578,6 @@ __global__ __launch_bounds__(NT, L2X2 ? SDDC_CHP_WAVES : 2) void r2iq_channels_p
     }
 }
 
-int g_occ[3][16] = {};
-int g_occ_p[4][8] = {};
-int g_cus = 0;
-
 struct ChLaunch {
     const int16_t *d_in;
     int nblk;
@@ -601,18 +597,12 @@ template <int D, bool RAND, bool CS16, bool COMPACT, bool STAGE_OK>
 hipError_t launch_v(const KernelTables &t, const ChLaunch &L)
 {
     auto kern = r2iq_channels_v2_kernel<D, RAND, CS16, COMPACT, STAGE_OK>;
-    int &occ = g_occ[D - 4][(STAGE_OK ? 8 : 0) + (RAND ? 4 : 0) + (CS16 ? 2 : 0) + (COMPACT ? 1 : 0)];
-    if (occ == 0) {
-        int nb = 0;
-        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, NT, 0);
-        if (e != hipSuccess) return e;
-        e = hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, L.device);
-        if (e != hipSuccess) return e;
-        occ = nb > 0 ? nb : 1;
-    }
+    int occ = 0, cus = 0;
+    hipError_t e = launch_geometry(t.lc, reinterpret_cast<const void *>(kern), NT, L.device, &occ, &cus);
+    if (e != hipSuccess) return e;
     const int nframes = L.nblk * FRAMES;
     const long long items = (long long)nframes * ((L.nch + CHUNK - 1) / CHUNK);
-    const int grid = (int)(items < (long long)g_cus * occ ? items : (long long)g_cus * occ);
+    const int grid = (int)(items < (long long)cus * occ ? items : (long long)cus * occ);
     float2 *scratch = grid <= L.scratch_rows ? L.scratch : nullptr;
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), 0, L.s, reinterpret_cast<const int *>(L.d_in), L.d_out,
                        L.stride / 2, nframes, L.d_tunebins, L.nch, t.tw_p1, t.rec_f, t.post8192, t.hsel[D], L.oa,
@@ -646,18 +636,12 @@ template <int D, bool RAND, bool CS16, bool L2X2>
 hipError_t launch_p2(const KernelTables &t, const ChLaunch &L)
 {
     auto kern = r2iq_channels_p_kernel<D, RAND, CS16, L2X2>;
-    int &occ = g_occ_p[D][(L2X2 ? 4 : 0) + (RAND ? 2 : 0) + (CS16 ? 1 : 0)];
-    if (occ == 0) {
-        int nb = 0;
-        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, NT, 0);
-        if (e != hipSuccess) return e;
-        e = hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, L.device);
-        if (e != hipSuccess) return e;
-        occ = nb > 0 ? nb : 1;
-    }
+    int occ = 0, cus = 0;
+    hipError_t e = launch_geometry(t.lc, reinterpret_cast<const void *>(kern), NT, L.device, &occ, &cus);
+    if (e != hipSuccess) return e;
     const int nframes = L.nblk * FRAMES;
     const long long items = (long long)nframes * ((L.nch + CHUNK_P - 1) / CHUNK_P);
-    const int grid = (int)(items < (long long)g_cus * occ ? items : (long long)g_cus * occ);
+    const int grid = (int)(items < (long long)cus * occ ? items : (long long)cus * occ);
     if constexpr (L2X2) {
         if (grid > L.scratch_rows) {   // one scratch row per workgroup: more workgroups than rows -> LDS form
             ChLaunch L0 = L;
@@ -681,11 +665,11 @@ hipError_t launch_p(const KernelTables &t, const ChLaunch &L)
     // the grid is at most CUs x 4 resident workgroups; the scratch holds L.scratch_rows rows
     if constexpr (SDDC_CHP_L2 && D >= 1) {
         if (L.scratch) {
-            if (g_cus == 0) {
-                hipError_t e = hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, L.device);
-                if (e != hipSuccess) return e;
-            }
-            if (g_cus * 4 <= L.scratch_rows) return launch_p2<D, RAND, CS16, true>(t, L);
+            int occ = 0, cus = 0;
+            hipError_t e = launch_geometry(t.lc, reinterpret_cast<const void *>(r2iq_channels_p_kernel<D, RAND, CS16, true>),
+                                           NT, L.device, &occ, &cus);
+            if (e != hipSuccess) return e;
+            if (cus * 4 <= L.scratch_rows) return launch_p2<D, RAND, CS16, true>(t, L);
         }
     }
     ChLaunch L0 = L;

@@ -9,6 +9,45 @@
 
 namespace sddc {
 
+// Launch geometry, per handle: the device's CU count and, per kernel (function pointer), the
+// resident workgroups per CU, queried on first use and kept in the handle (all launches run
+// under the handle's lock), so no launch path writes namespace-scope state.
+struct LaunchCache {
+    static constexpr int kSlots = 256;
+    int cus = 0;
+    int n = 0;
+    const void *fn[kSlots] = {};
+    int occ[kSlots] = {};
+};
+
+// occ = resident workgroups per CU of kernel fn (`threads` per workgroup, static LDS), cus = the
+// device's CUs; cached in *lc when lc is non-null.
+inline hipError_t launch_geometry(LaunchCache *lc, const void *fn, int threads, int device, int *occ, int *cus)
+{
+    if (lc) {
+        for (int i = 0; i < lc->n; i++)
+            if (lc->fn[i] == fn) {
+                *occ = lc->occ[i];
+                *cus = lc->cus;
+                return hipSuccess;
+            }
+    }
+    int nb = 0, c = 0;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, threads, 0);
+    if (e != hipSuccess) return e;
+    e = hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, device);
+    if (e != hipSuccess) return e;
+    *occ = nb > 0 ? nb : 1;
+    *cus = c;
+    if (lc && lc->n < LaunchCache::kSlots) {
+        lc->cus = c;
+        lc->fn[lc->n] = fn;
+        lc->occ[lc->n] = *occ;
+        lc->n++;
+    }
+    return hipSuccess;
+}
+
 // Device-resident constant tables, built once per handle (the reference's
 // fft_mt_r2iq::Init builds filterHw and the FFTW plans, fft_mt_r2iq.cpp:147-227).
 // All twiddles are evaluated in double on the host and rounded once to float.
@@ -23,6 +62,7 @@ struct KernelTables {
     const float2 *rec_i[7] = {};       // [2][256]: W_N^{j}, W_N^{4j}        inverse pass 2 (N >= 512)
     const float2 *twf64 = nullptr;     // [64][64]: W_4096^{L q} at [q][L]  wave kernel F1 twiddles (d = 0,
                                        // libsddc_ddc_variants.so)
+    LaunchCache *lc = nullptr;         // the handle's launch geometry (written under the handle's lock)
 };
 
 // v2 (default): persistent workgroups, input prefetch, swizzled LDS.  pq: the split x filter
@@ -44,9 +84,13 @@ hipError_t launch_build_split_filter(const KernelTables &t, int d, int tunebin, 
 #endif
 bool fs_path(int d, int tunebin);
 hipError_t launch_build_fs_tables(const KernelTables &t, int tunebin, float4 *pqf, float2 *fsl, hipStream_t s);
+// wq: a zeroed slot of kFsQueueWords unsigned words (the dynamic frame queue); the launch leaves it
+// zeroed again.  Launches that may run at the same time need different slots.
+constexpr int kFsQueueWords = 16 * 9;
 hipError_t launch_frames_fs(const KernelTables &t, const int16_t *d_in, int nblk, void *d_out, const float4 *pqf,
                             const float2 *fsl, int tunebin, int lsb, int rand, int cs16, float cs16_scale,
-                            const float2 *nco_starts, const float2 *nco_trig, int device, hipStream_t s);
+                            const float2 *nco_starts, const float2 *nco_trig, unsigned *wq, int device,
+                            hipStream_t s);
 
 // many-channel v2 (d = 4..6): persistent, forward once per (frame, 128-channel chunk)
 // stride: scalar components (float or int16) per channel row; cs16 as above.  d_windows:

@@ -491,6 +491,46 @@ __device__ __forceinline__ void emit_frame_q(void *__restrict__ out, int fbase, 
 }
 
 
+// Dynamic frame distribution.  With a static split (each workgroup a fixed contiguous range)
+// the four workgroups of a CU finish far apart: the SIMDs arbitrate by age, so the first-
+// dispatched workgroup of a CU runs ~1.6x faster than the last, and the CU spends the last
+// ~40 % of the launch with 3, 2, then 1 workgroup resident (s_memtime / s_memrealtime stamps
+// by HW_ID slot, profiles/r03/stamps).  Frames are handed out one at a time instead: 8 shards
+// of consecutive frames (one counter each, on its own 64-B line; a workgroup starts on shard
+// blockIdx % 8 and moves on when it runs dry), so consecutive frames, which share 2048 input
+// samples, mostly stay in one XCD's L2.  Thread 0 takes a ticket for the next frame at the start
+// of the current one and looks at it only before inverse pass 0's stores (the answer is needed
+// at inverse pass 1, for the next frame's input prefetch): waiting for the atomic where it is
+// issued cost wave 0 ~1800 cycles per frame (profiles/r03/stamps/stamps_q.txt).
+// wq: this launch's slot of the handle's queue ring, zero at entry; the last workgroup to leave
+// clears it for the slot's next launch (the counters are touched only by device-scope atomics).
+constexpr int FS_SHARDS = 8;
+static_assert(kFsQueueWords == 16 * (FS_SHARDS + 1), "queue slot: one 64-B line per shard counter + the done count");
+__device__ __forceinline__ int fs_shard_lo(int nframes, int s) { return (int)(((long long)nframes * s) / FS_SHARDS); }
+// the ticket of shard (sh0 + shn) mod 8; its value is looked at only by fs_resolve, so the wave
+// does not wait for the atomic where it is issued
+__device__ __forceinline__ unsigned fs_ticket(unsigned *wq, int sh0, int shn)
+{
+    return shn < FS_SHARDS ? atomicAdd(wq + 16 * ((sh0 + shn) & (FS_SHARDS - 1)), 1u) : 0u;
+}
+// the frame of a ticket, or (its shard run dry) the next shards' tickets in turn; -1 when all are
+__device__ __forceinline__ int fs_resolve(unsigned *wq, int nframes, int sh0, int &shn, unsigned ticket)
+{
+    while (shn < FS_SHARDS) {
+        const int s = (sh0 + shn) & (FS_SHARDS - 1);
+        const int lo = fs_shard_lo(nframes, s), hi = fs_shard_lo(nframes, s + 1);
+        if ((int)ticket < hi - lo) return lo + (int)ticket;
+        if (++shn < FS_SHARDS) ticket = fs_ticket(wq, sh0, shn);
+    }
+    return -1;
+}
+__device__ __forceinline__ void fs_queue_done(unsigned *wq, unsigned grid)
+{
+    if (atomicAdd(wq + 16 * FS_SHARDS, 1u) == grid - 1) {
+        for (int s = 0; s <= FS_SHARDS; s++) atomicExch(wq + 16 * s, 0u);
+    }
+}
+
 // Diagnostic build (-DSDDC_STAMPS, tools/fs_stamps.py; never the product): per wave, the cycles
 // (s_memtime) of each work segment between two barriers and of each barrier wait, summed over
 // the workgroup's frames in SGPRs, and written once at the end by lane 0 (vector stores) to a
@@ -499,18 +539,16 @@ __device__ __forceinline__ void emit_frame_q(void *__restrict__ out, int fbase, 
 #ifndef SDDC_FS_PQ
 #define SDDC_FS_PQ 1   // (P, Q) bin pairs the FS kernel's split loads run ahead of their use
 #endif
-#ifndef SDDC_FS_PF
-#define SDDC_FS_PF 1   // where the FS kernel issues the next frame's input loads: 0 pass 0, 1 inverse pass 1
-#endif
 constexpr int kFsSegs = 9;                         // work segments: 8 barriers + the frame tail
-constexpr int kFsStampWords = 2 * kFsSegs + 4;     // work[9], wait[9] (wait[8] unused), frames, ticks, rt lo/hi
+// work[9], wait[9] (wait[8] unused), frames, ticks, realtime ticks, build, realtime start, end, HW_ID
+constexpr int kFsStampWords = 2 * kFsSegs + 7;
 #ifdef SDDC_STAMPS
 // SDDC_STAMPS = 1 stamps barriers 0..3, = 2 barriers 4..7 (all eight in one build spill: the
 // accumulators live in SGPRs); the time of an unstamped barrier falls into the next work segment.
 __device__ unsigned g_fs_stamps[2048 * 4 * kFsStampWords];
 constexpr int kStLo = SDDC_STAMPS == 2 ? 4 : 0;
 #define FS_STAMP_INIT()                                                                              \
-    unsigned st_work[kFsSegs] = {}, st_wait[kFsSegs] = {};                                         \
+    unsigned st_work[kFsSegs] = {}, st_wait[kFsSegs] = {}, st_frames = 0;                          \
     unsigned long long st_t = __builtin_amdgcn_s_memtime(), st_a = st_t;                          \
     const unsigned long long st_t0 = st_t, st_r0 = __builtin_amdgcn_s_memrealtime()
 #define FS_SYNC(i)                                                                                   \
@@ -530,6 +568,7 @@ constexpr int kStLo = SDDC_STAMPS == 2 ? 4 : 0;
         st_a = __builtin_amdgcn_s_memtime();                                                         \
         st_work[kFsSegs - 1] += (unsigned)(st_a - st_t);                                             \
         st_t = st_a;                                                                                 \
+        st_frames++;                                                                                 \
     } while (0)
 #define FS_STAMP_WRITE(wg, tid, nfr)                                                                 \
     do {                                                                                             \
@@ -544,6 +583,9 @@ constexpr int kStLo = SDDC_STAMPS == 2 ? 4 : 0;
             o[2 * kFsSegs + 1] = (unsigned)(st_t - st_t0);                                           \
             o[2 * kFsSegs + 2] = (unsigned)(st_r1 - st_r0);                                          \
             o[2 * kFsSegs + 3] = (unsigned)SDDC_STAMPS;                                              \
+            o[2 * kFsSegs + 4] = (unsigned)st_r0;                                                    \
+            o[2 * kFsSegs + 5] = (unsigned)st_r1;                                                    \
+            o[2 * kFsSegs + 6] = __builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));             \
         }                                                                                            \
     } while (0)
 #else
@@ -558,7 +600,8 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
     const int *__restrict__ in32, void *__restrict__ out, int nframes,
     const float2 *__restrict__ tw_p1, const float2 *__restrict__ tw_q1,
     const float2 *__restrict__ rec_f, const float2 *__restrict__ tw4096,
-    const float4 *__restrict__ pqf, const float2 *__restrict__ fsl, int tunebin, OutArgs oa, NcoArgs nco)
+    const float4 *__restrict__ pqf, const float2 *__restrict__ fsl, int tunebin, OutArgs oa, NcoArgs nco,
+    unsigned *__restrict__ wq)
 {
     __shared__ __attribute__((aligned(16))) float2 lds[HALF];
     // pass-1 twiddles W_256^{s r} [15][16] (the inverse pass conjugates them: at d = 0 its table is
@@ -570,11 +613,13 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
     __shared__ __attribute__((aligned(16))) float2 wtab[2 * NT];
     __shared__ __attribute__((aligned(16))) float2 gtab[NT];
 
+    __shared__ int s_next;   // the workgroup's next frame (thread 0's dequeue), -1 when none is left
+
     const int tid = (int)threadIdx.x;
-    const int G = (int)gridDim.x, w = (int)blockIdx.x;
-    const int f0 = (int)(((long long)nframes * w) / G);
-    const int f1 = (int)(((long long)nframes * (w + 1)) / G);
-    if (f0 >= f1) return;
+    const int w = (int)blockIdx.x;
+    const int sh0 = w & (FS_SHARDS - 1);   // home shard (blockIdx % 8: the XCD under round-robin placement)
+    int shn = 0;                           // thread 0: shards found empty so far
+    if (tid == 0) s_next = fs_resolve(wq, nframes, sh0, shn, fs_ticket(wq, sh0, shn));
 
     // per-lane constants: the column, and (reloaded every frame from L2, to keep them out of
     // the registers of the other passes) the twiddle bases of the two NS = 256 passes
@@ -590,12 +635,14 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
     const bool w0 = __builtin_amdgcn_readfirstlane(tid >> 6) == 0;   // the wave holding columns 0, 128
 #endif
 
-    int blk = f0 / FRAMES, k = f0 - blk * FRAMES;
+    __syncthreads();
+    int f = s_next;
+    int blk = f / FRAMES, k = f - blk * FRAMES;
     int x[16];
-    load_frame(in32, blk, k, x);
+    if (f >= 0) load_frame(in32, blk, k, x);
     FS_STAMP_INIT();
 
-    for (int f = f0; f < f1; f++) {
+    while (f >= 0) {
         int z = 0;
         asm volatile("" : "+s"(z));
         const int t = tid + z;
@@ -616,15 +663,11 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
                 } else {
                     a[r] = make_float2((float)(int)(short)(x[r] & 0xffff), (float)(x[r] >> 16));
                 }
-            if (++k == FRAMES) {
-                k = 0;
-                ++blk;
-            }
-#if SDDC_FS_PF == 0
-            if (f + 1 < f1) load_frame(in32, blk, k, x);   // prefetch the next frame
-#endif
             dft16<-1>(a, v);
         }
+        // thread 0 asks for the frame after this one now; the answer is needed by inverse pass 1
+        unsigned nq = 0;
+        if (tid == 0) nq = fs_ticket(wq, sh0, shn);
         FS_SYNC(0);   // the previous frame's last LDS reads are done
 #pragma unroll
         for (int r = 0; r < 16; r++) lds[16 * t + (r ^ x15)] = v[r];
@@ -667,9 +710,6 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
             twiddle_rec16<-1>(a, fw1, fw4);
             dft16<-1>(a, v);
         }
-#if SDDC_FS_PF == 3
-        if (f + 1 < f1) load_frame(in32, blk, k, x);   // the next frame's input
-#endif
         // ---- split x filter (bins c + 256 k, mirror from the partner lane) -> inverse pass 0 ----
         float2 u[16];
         {
@@ -714,22 +754,32 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
         }
         FS_SYNC(4);   // every wave's pass-2 reads are done
         {
-            const unsigned xc0 = 128u * (unsigned)c + 8u * (unsigned)(c & 15);   // row 16 c + (r ^ (c & 15))
+            // row 16 c + (r ^ (swz(c) & 15)): the key XORs in c >> 4 so that the lane pairs c, -c
+            // (equal c mod 16 for c = 0, 8 mod 16) never share a bank (tools/fs_perm.py)
+            const unsigned xc0 = 128u * (unsigned)c + 8u * (unsigned)(swz(c) & 15);
 #pragma unroll
             for (int r = 0; r < 16; r++) st_row(lds, xc0, r, 0, u[r]);
         }
+        if (tid == 0) s_next = fs_resolve(wq, nframes, sh0, shn, nq);
         FS_SYNC(5);
-#if SDDC_FS_PF == 1
         // the next frame's input: issued here rather than in pass 0, so its 16 registers are
         // free through forward pass 2 and the split, and the loads' waits never hold pass 2
-        if (f + 1 < f1) load_frame(in32, blk, k, x);
-#endif
+        const int fn = s_next;
+        if (fn >= 0) {
+            blk = fn / FRAMES;
+            k = fn - blk * FRAMES;
+            load_frame(in32, blk, k, x);
+        }
         // ---- inverse pass 1 (R16, NS16): table twiddles W_256^{-(t%16) r} ----
         // inverse pass 2's bases: W^t, W^{4t} and the lane's modulation factor g_t
         {
             float2 a[16];
+            // element j + 256 r was stored by inverse pass-0 column (j >> 4) + 16 r under the key
+            // swz(column) & 15 = (j >> 4) ^ r: byte (8 sT ^ 8 r) + 2048 r, one v_xor per read
+            const unsigned sT8 = 8u * (unsigned)sT;
 #pragma unroll
-            for (int r = 0; r < 16; r++) XRD(a[r], lds[sT + NT * r]);
+            for (int r = 0; r < 16; r++)
+                XRD(a[r], *reinterpret_cast<const float2 *>(reinterpret_cast<const char *>(lds) + ((sT8 ^ (8u * r)) + 2048u * r)));
             table_twiddle<+1, true>(a, twl, 16, x15);
             dft16<+1>(a, u);
         }
@@ -744,9 +794,6 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
             for (int r = 0; r < 16; r++) lds[b1 + 16 * r + (y15 ^ r)] = u[r];
         }
         FS_SYNC(7);
-#if SDDC_FS_PF == 2
-        if (f + 1 < f1) load_frame(in32, blk, k, x);   // the next frame's input
-#endif
         // ---- inverse pass 2 (R16, NS256): twiddles g_t W^{-t r}, quarter turns, overlap-discard ----
         {
             float2 a[16];
@@ -764,8 +811,10 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
             }
         }
         FS_STAMP_FRAME_END();
+        f = fn;
     }
-    FS_STAMP_WRITE(w, tid, f1 - f0);
+    FS_STAMP_WRITE(w, tid, st_frames);
+    if (tid == 0) fs_queue_done(wq, (unsigned)gridDim.x);
 }
 
 // FS tables of one tunebin: pqf[l + 256 k] = (P, Q) of bin b = kFsPerm[l] + 256 k (inverse input
@@ -823,9 +872,6 @@ __global__ void build_split_filter_kernel(const float2 *__restrict__ hsel, const
     pq[m] = c;
 }
 
-int g_occupancy[7][8] = {};
-int g_cus = 0;
-
 struct Launch {
     const int16_t *d_in;
     int nblk;
@@ -842,19 +888,11 @@ template <int D, bool RAND, bool NCO, bool CS16>
 hipError_t launch_v(const KernelTables &t, const Launch &L)
 {
     auto kern = r2iq_persistent_kernel<D, RAND, NCO, CS16>;
-    int &occ = g_occupancy[D][(RAND ? 4 : 0) + (NCO ? 2 : 0) + (CS16 ? 1 : 0)];
-    if (occ == 0) {
-        int nb = 0;
-        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, NT, 0);
-        if (e != hipSuccess) return e;
-        int cus = 0;
-        e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, L.device);
-        if (e != hipSuccess) return e;
-        g_cus = cus;
-        occ = nb > 0 ? nb : 1;
-    }
+    int occ = 0, cus = 0;
+    hipError_t e = launch_geometry(t.lc, reinterpret_cast<const void *>(kern), NT, L.device, &occ, &cus);
+    if (e != hipSuccess) return e;
     const int nframes = L.nblk * FRAMES;
-    int grid = g_cus * occ;
+    int grid = cus * occ;
     if (grid > nframes) grid = nframes;
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), 0, L.s, reinterpret_cast<const int *>(L.d_in),
                        L.d_out, nframes, t.tw_p1, t.tw_q1[D], t.rec_f, t.rec_i[D], t.tw4096, L.pq, L.tunebin, L.oa,
@@ -862,28 +900,19 @@ hipError_t launch_v(const KernelTables &t, const Launch &L)
     return hipGetLastError();
 }
 
-int g_occupancy_fs[8] = {};
-
 template <bool RAND, bool NCO, bool CS16>
-hipError_t launch_fs_v(const KernelTables &t, const Launch &L, const float4 *pqf, const float2 *fsl)
+hipError_t launch_fs_v(const KernelTables &t, const Launch &L, const float4 *pqf, const float2 *fsl, unsigned *wq)
 {
     auto kern = r2iq_fs_kernel<RAND, NCO, CS16>;
-    int &occ = g_occupancy_fs[(RAND ? 4 : 0) + (NCO ? 2 : 0) + (CS16 ? 1 : 0)];
-    if (occ == 0) {
-        int nb = 0;
-        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, NT, 0);
-        if (e != hipSuccess) return e;
-        int cus = 0;
-        e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, L.device);
-        if (e != hipSuccess) return e;
-        g_cus = cus;
-        occ = nb > 0 ? nb : 1;
-    }
+    int occ = 0, cus = 0;
+    hipError_t e = launch_geometry(t.lc, reinterpret_cast<const void *>(kern), NT, L.device, &occ, &cus);
+    if (e != hipSuccess) return e;
     const int nframes = L.nblk * FRAMES;
-    int grid = g_cus * occ;
+    int grid = cus * occ;
     if (grid > nframes) grid = nframes;
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), 0, L.s, reinterpret_cast<const int *>(L.d_in),
-                       L.d_out, nframes, t.tw_p1, t.tw_q1[0], t.rec_f, t.tw4096, pqf, fsl, L.tunebin, L.oa, L.nco);
+                       L.d_out, nframes, t.tw_p1, t.tw_q1[0], t.rec_f, t.tw4096, pqf, fsl, L.tunebin, L.oa, L.nco,
+                       wq);
     return hipGetLastError();
 }
 
@@ -933,18 +962,18 @@ hipError_t launch_build_fs_tables(const KernelTables &t, int tunebin, float4 *pq
 
 hipError_t launch_frames_fs(const KernelTables &t, const int16_t *d_in, int nblk, void *d_out, const float4 *pqf,
                             const float2 *fsl, int tunebin, int lsb, int rand, int cs16, float cs16_scale,
-                            const float2 *nco_starts, const float2 *nco_trig, int device, hipStream_t s)
+                            const float2 *nco_starts, const float2 *nco_trig, unsigned *wq, int device, hipStream_t s)
 {
     if (tunebin & 3) return hipErrorInvalidValue;
     const Launch L{d_in, nblk, d_out, nullptr, tunebin, device, s, OutArgs{lsb ? 0x80000000u : 0u, cs16_scale},
                    NcoArgs{nco_starts, nco_trig}};
     const bool nco = nco_starts != nullptr;
     if (rand) {
-        if (nco) return cs16 ? launch_fs_v<true, true, true>(t, L, pqf, fsl) : launch_fs_v<true, true, false>(t, L, pqf, fsl);
-        return cs16 ? launch_fs_v<true, false, true>(t, L, pqf, fsl) : launch_fs_v<true, false, false>(t, L, pqf, fsl);
+        if (nco) return cs16 ? launch_fs_v<true, true, true>(t, L, pqf, fsl, wq) : launch_fs_v<true, true, false>(t, L, pqf, fsl, wq);
+        return cs16 ? launch_fs_v<true, false, true>(t, L, pqf, fsl, wq) : launch_fs_v<true, false, false>(t, L, pqf, fsl, wq);
     }
-    if (nco) return cs16 ? launch_fs_v<false, true, true>(t, L, pqf, fsl) : launch_fs_v<false, true, false>(t, L, pqf, fsl);
-    return cs16 ? launch_fs_v<false, false, true>(t, L, pqf, fsl) : launch_fs_v<false, false, false>(t, L, pqf, fsl);
+    if (nco) return cs16 ? launch_fs_v<false, true, true>(t, L, pqf, fsl, wq) : launch_fs_v<false, true, false>(t, L, pqf, fsl, wq);
+    return cs16 ? launch_fs_v<false, false, true>(t, L, pqf, fsl, wq) : launch_fs_v<false, false, false>(t, L, pqf, fsl, wq);
 }
 
 hipError_t launch_frames_persistent(const KernelTables &t, int d, const int16_t *d_in, int nblk, void *d_out,

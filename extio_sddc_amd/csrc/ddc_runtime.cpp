@@ -169,6 +169,7 @@ struct sddc_ddc {
     int out_fmt = SDDC_DDC_FMT_CF32;       // output stage format
     float cs16_scale = 1.f;
     sddc::KernelTables tables;
+    sddc::LaunchCache launch_cache;        // per-kernel resident workgroups and CUs of this device
     float2 *d_tables = nullptr;
 
     mutable std::mutex mu;                 // serialises the host path and buffer growth
@@ -207,6 +208,12 @@ struct sddc_ddc {
     // the d = 0 fused-split kernel's per-tunebin tables: pqf (4096 float4) then fsl (768 float2)
     float4 *d_fs = nullptr;
     int fs_tb = -1;
+    // the fused-split kernel's dynamic frame queues: a ring of kQueueSlots zeroed slots, one per
+    // launch in turn (each launch leaves its slot zeroed; the ring lets launches on different
+    // streams overlap)
+    static constexpr int kQueueSlots = 64;
+    unsigned *d_queue = nullptr;
+    int queue_slot = 0;
     Readers readers;
 
     // fused fine-tune NCO: host chain + per-launch [T | lane starts] staged through a
@@ -374,6 +381,10 @@ int sddc_ddc_create(float gain, int device, sddc_ddc_t **out)
     if (e == hipSuccess) e = hipMalloc(&h->d_pq, SDDC_DDC_HALF_FFT * sizeof(float4));
     if (e == hipSuccess) e = hipMalloc(&h->d_wave, 4096 * (sizeof(float4) + sizeof(float2)));
     if (e == hipSuccess) e = hipMalloc(&h->d_fs, 4096 * sizeof(float4) + 768 * sizeof(float2));
+    if (e == hipSuccess)
+        e = hipMalloc(&h->d_queue, (size_t)sddc_ddc::kQueueSlots * sddc::kFsQueueWords * sizeof(unsigned));
+    if (e == hipSuccess)
+        e = hipMemset(h->d_queue, 0, (size_t)sddc_ddc::kQueueSlots * sddc::kFsQueueWords * sizeof(unsigned));
     if (e != hipSuccess) {
         sddc_ddc_destroy(h);
         return fail(SDDC_ERR_HIP, "create: %s", hipGetErrorString(e));
@@ -384,6 +395,7 @@ int sddc_ddc_create(float gain, int device, sddc_ddc_t **out)
     h->tables.tw_p1 = T + o_p1;
     h->tables.rec_f = T + o_recf;
     h->tables.twf64 = T + o_twf64;
+    h->tables.lc = &h->launch_cache;
     for (int d = 0; d < SDDC_DDC_NDEC; d++) {
         h->tables.hsel[d] = T + o_hsel[d];
         h->tables.tw_q1[d] = T + o_q1[d];
@@ -409,6 +421,9 @@ int sddc_ddc_destroy(sddc_ddc_t *h)
     {
         DeviceGuard g(h->device);
         if (h->stream) (void)hipStreamSynchronize(h->stream);
+        // launches on the callers' streams may still read the tables below: wait for them first
+        (void)h->readers.sync();
+        (void)h->ch_readers.sync();
         if (h->d_tables) (void)hipFree(h->d_tables);
         for (auto &sl : h->hs) {
             if (sl.d_in) (void)hipFree(sl.d_in);
@@ -427,8 +442,7 @@ int sddc_ddc_destroy(sddc_ddc_t *h)
         if (h->d_pq) (void)hipFree(h->d_pq);
         if (h->d_wave) (void)hipFree(h->d_wave);
         if (h->d_fs) (void)hipFree(h->d_fs);
-        (void)h->readers.sync();
-        (void)h->ch_readers.sync();
+        if (h->d_queue) (void)hipFree(h->d_queue);
         h->readers.clear();
         h->ch_readers.clear();
         for (int i = 0; i < sddc_ddc::kNcoSlots; i++) {
@@ -607,9 +621,11 @@ static hipError_t launch_single(sddc_ddc_t *h, const int16_t *d_in, int nblk, vo
             if (e != hipSuccess) return e;
             h->fs_tb = h->tunebin;
         }
+        unsigned *wq = h->d_queue + (size_t)h->queue_slot * sddc::kFsQueueWords;
+        h->queue_slot = (h->queue_slot + 1) % sddc_ddc::kQueueSlots;
         hipError_t e = sddc::launch_frames_fs(h->tables, d_in, nblk, d_out, pqf, fsl, h->tunebin, h->lsb, h->rand,
                                               h->out_fmt == SDDC_DDC_FMT_CS16, h->cs16_scale, nco_starts, nco_trig,
-                                              h->device, s);
+                                              wq, h->device, s);
         if (e != hipSuccess) return e;
         return h->readers.record(s);
     }

@@ -263,25 +263,17 @@ __global__ __launch_bounds__(NTP, 8) void r2iq_pair_kernel(
     }
 }
 
-int g_cus = 0;
-int g_occ[8] = {};
 
 template <bool RAND, bool NCO, bool CS16>
 hipError_t launch_pair(const KernelTables &t, const int16_t *d_in, int nblk, void *d_out, const float4 *pq,
                        int tunebin, OutArgs oa, NcoArgs nco, int device, hipStream_t s)
 {
     auto kern = r2iq_pair_kernel<RAND, NCO, CS16>;
-    int &occ = g_occ[(RAND ? 4 : 0) + (NCO ? 2 : 0) + (CS16 ? 1 : 0)];
-    if (occ == 0) {
-        int nb = 0;
-        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, NTP, 0);
-        if (e != hipSuccess) return e;
-        e = hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, device);
-        if (e != hipSuccess) return e;
-        occ = nb > 0 ? nb : 1;
-    }
+    int occ = 0, cus = 0;
+    hipError_t e = launch_geometry(t.lc, reinterpret_cast<const void *>(kern), NTP, device, &occ, &cus);
+    if (e != hipSuccess) return e;
     const int nframes = nblk * FRAMES;
-    int grid = g_cus * occ;
+    int grid = cus * occ;
     if (grid > nframes) grid = nframes;
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NTP), 0, s, reinterpret_cast<const int *>(d_in), d_out,
                        nframes, t.tw_p1, t.rec_f, t.post8192, pq, tunebin, oa, nco);

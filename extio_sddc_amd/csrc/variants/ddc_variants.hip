@@ -352,7 +352,6 @@ __global__ __launch_bounds__(NT8, SDDC_R8_WAVES) void r2iq_r8_kernel(
     }
 }
 
-int g_cus = 0;
 
 struct Launch {
     const int16_t *d_in;
@@ -366,23 +365,16 @@ struct Launch {
     NcoArgs nco;
 };
 
-int g_pipe_occ[8] = {};
 
 template <bool RAND, bool NCO, bool CS16>
 hipError_t launch_pipe(const KernelTables &t, const Launch &L)
 {
     auto kern = r2iq_pipe_kernel<RAND, NCO, CS16>;
-    int &occ = g_pipe_occ[(RAND ? 4 : 0) + (NCO ? 2 : 0) + (CS16 ? 1 : 0)];
-    if (occ == 0) {
-        int nb = 0;
-        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, NT, 0);
-        if (e != hipSuccess) return e;
-        e = hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, L.device);
-        if (e != hipSuccess) return e;
-        occ = nb > 0 ? nb : 1;
-    }
+    int occ = 0, cus = 0;
+    hipError_t e = launch_geometry(t.lc, reinterpret_cast<const void *>(kern), NT, L.device, &occ, &cus);
+    if (e != hipSuccess) return e;
     const int nframes = L.nblk * FRAMES;
-    int grid = g_cus * occ;
+    int grid = cus * occ;
     if (grid > nframes) grid = nframes;
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), 0, L.s, reinterpret_cast<const int *>(L.d_in), L.d_out,
                        nframes, t.tw_p1, t.tw_q1[0], t.rec_f, L.pq, L.tunebin, L.oa, L.nco);
@@ -395,23 +387,16 @@ hipError_t launch_pipe_f(const KernelTables &t, const Launch &L, bool cs16)
     return cs16 ? launch_pipe<RAND, NCO, true>(t, L) : launch_pipe<RAND, NCO, false>(t, L);
 }
 
-int g_r8_occ[8] = {};
 
 template <bool RAND, bool NCO, bool CS16>
 hipError_t launch_r8(const KernelTables &t, const Launch &L)
 {
     auto kern = r2iq_r8_kernel<RAND, NCO, CS16>;
-    int &occ = g_r8_occ[(RAND ? 4 : 0) + (NCO ? 2 : 0) + (CS16 ? 1 : 0)];
-    if (occ == 0) {
-        int nb = 0;
-        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, NT8, 0);
-        if (e != hipSuccess) return e;
-        e = hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, L.device);
-        if (e != hipSuccess) return e;
-        occ = nb > 0 ? nb : 1;
-    }
+    int occ = 0, cus = 0;
+    hipError_t e = launch_geometry(t.lc, reinterpret_cast<const void *>(kern), NT8, L.device, &occ, &cus);
+    if (e != hipSuccess) return e;
     const int nframes = L.nblk * FRAMES;
-    int grid = g_cus * occ;
+    int grid = cus * occ;
     if (grid > nframes) grid = nframes;
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT8), 0, L.s, reinterpret_cast<const int *>(L.d_in), L.d_out,
                        nframes, t.post8192, L.pq, L.tunebin, L.oa, L.nco);

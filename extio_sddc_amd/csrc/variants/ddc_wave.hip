@@ -404,30 +404,19 @@ __global__ void build_wave_tables_kernel(const float2 *__restrict__ hsel, const 
     twI[idx] = make_float2((float)cos(a), (float)sin(a));
 }
 
-int g_wocc[8] = {};
-int g_wcus = 0;
-
 template <bool RAND, bool NCO, bool CS16>
 hipError_t launch_w(const float2 *twF, const float4 *pqW, const float2 *twI, const int16_t *d_in, int nblk,
-                    void *d_out, int tunebin, OutArgs oa, NcoArgs nco, int device, hipStream_t s)
+                    void *d_out, int tunebin, OutArgs oa, NcoArgs nco, int device, hipStream_t s, LaunchCache *lc)
 {
     auto kern = r2iq_wave_kernel<RAND, NCO, CS16>;
-    int &occ = g_wocc[(RAND ? 4 : 0) + (NCO ? 2 : 0) + (CS16 ? 1 : 0)];
-    if (occ == 0) {
-        int nb = 0;
-        hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, 64, 0);
-        if (e != hipSuccess) return e;
-        int cus = 0;
-        e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
-        if (e != hipSuccess) return e;
-        g_wcus = cus;
-        occ = nb > 0 ? nb : 1;
+    int occ = 0, cus = 0;
+    hipError_t e = launch_geometry(lc, reinterpret_cast<const void *>(kern), 64, device, &occ, &cus);
+    if (e != hipSuccess) return e;
 #ifdef SDDC_WV_OCC
-        occ = occ < SDDC_WV_OCC ? occ : SDDC_WV_OCC;   // A/B builds: resident waves per CU
+    occ = occ < SDDC_WV_OCC ? occ : SDDC_WV_OCC;   // A/B builds: resident waves per CU
 #endif
-    }
     const int nframes = nblk * FRAMES;
-    int grid = g_wcus * occ;
+    int grid = cus * occ;
     if (grid > nframes) grid = nframes;
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64), 0, s, reinterpret_cast<const int *>(d_in), d_out,
                        nframes, twF, pqW, twI, tunebin, oa, nco);
@@ -436,10 +425,11 @@ hipError_t launch_w(const float2 *twF, const float4 *pqW, const float2 *twI, con
 
 template <bool RAND, bool NCO>
 hipError_t launch_wc(const float2 *twF, const float4 *pqW, const float2 *twI, const int16_t *d_in, int nblk,
-                     void *d_out, int tunebin, OutArgs oa, NcoArgs nco, bool cs16, int device, hipStream_t s)
+                     void *d_out, int tunebin, OutArgs oa, NcoArgs nco, bool cs16, int device, hipStream_t s,
+                     LaunchCache *lc)
 {
-    return cs16 ? launch_w<RAND, NCO, true>(twF, pqW, twI, d_in, nblk, d_out, tunebin, oa, nco, device, s)
-                : launch_w<RAND, NCO, false>(twF, pqW, twI, d_in, nblk, d_out, tunebin, oa, nco, device, s);
+    return cs16 ? launch_w<RAND, NCO, true>(twF, pqW, twI, d_in, nblk, d_out, tunebin, oa, nco, device, s, lc)
+                : launch_w<RAND, NCO, false>(twF, pqW, twI, d_in, nblk, d_out, tunebin, oa, nco, device, s, lc);
 }
 
 }  // namespace
@@ -460,10 +450,10 @@ hipError_t launch_frames_wave(const KernelTables &t, const int16_t *d_in, int nb
     const NcoArgs nco{nco_starts, nco_trig};
     const bool c = cs16 != 0, n = nco_starts != nullptr;
     if (rand)
-        return n ? launch_wc<true, true>(t.twf64, pqW, twI, d_in, nblk, d_out, tunebin, oa, nco, c, device, s)
-                 : launch_wc<true, false>(t.twf64, pqW, twI, d_in, nblk, d_out, tunebin, oa, nco, c, device, s);
-    return n ? launch_wc<false, true>(t.twf64, pqW, twI, d_in, nblk, d_out, tunebin, oa, nco, c, device, s)
-             : launch_wc<false, false>(t.twf64, pqW, twI, d_in, nblk, d_out, tunebin, oa, nco, c, device, s);
+        return n ? launch_wc<true, true>(t.twf64, pqW, twI, d_in, nblk, d_out, tunebin, oa, nco, c, device, s, t.lc)
+                 : launch_wc<true, false>(t.twf64, pqW, twI, d_in, nblk, d_out, tunebin, oa, nco, c, device, s, t.lc);
+    return n ? launch_wc<false, true>(t.twf64, pqW, twI, d_in, nblk, d_out, tunebin, oa, nco, c, device, s, t.lc)
+             : launch_wc<false, false>(t.twf64, pqW, twI, d_in, nblk, d_out, tunebin, oa, nco, c, device, s, t.lc);
 }
 
 }  // namespace sddc

@@ -64,7 +64,10 @@ def broadcast_samples(buf, src: int = 0, method: str = "sag", async_op: bool = F
     last = None
     if piece:
         pieces = list(w32[: piece * world].view(world, piece).unbind(0))
-        mine = pieces[rank]
+        # the root receives its own piece into a scratch copy rather than into the slice its
+        # scatter_list reads (no aliased send/receive buffers on any backend); every other rank
+        # receives in place, which the all-gather below then reads in place
+        mine = pieces[rank] if rank != src else torch.empty_like(pieces[rank])
         # RCCL runs one rank's collectives in issue order on its stream; gloo may run queued
         # async collectives concurrently, so there the scatter completes first
         sw = dist.scatter(mine, scatter_list=pieces if rank == src else None, src=src, async_op=async_op)

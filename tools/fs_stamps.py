@@ -87,6 +87,20 @@ def main():
         clk = np.median(ticks[ok] / (rt[ok] * 1e-8)) / 1e9
         print(f"\n{os.path.basename(lib)} (stamps build {which}): {ms:.4f} ms/launch, in-kernel clock {clk:.3f} GHz, "
               f"{np.median(ticks[ok] / fr[ok]):.0f} cycles per frame per wave (median)")
+        rs = st[:, 0, 2 * SEGS + 4].astype(np.int64)
+        re = st[:, 0, 2 * SEGS + 5].astype(np.int64)
+        hw = st[:, 0, 2 * SEGS + 6].astype(np.int64)
+        tg = (hw >> 16) & 15
+        t0 = rs.min()
+        rs_us, re_us = (rs - t0) * 0.01, (re - t0) * 0.01
+        print(f"  workgroup start (us after the first): p50 {np.median(rs_us):.2f} max {rs_us.max():.2f}; "
+              f"end: min {re_us.min():.1f} p10 {np.percentile(re_us, 10):.1f} p50 {np.median(re_us):.1f} "
+              f"p90 {np.percentile(re_us, 90):.1f} max {re_us.max():.1f}")
+        for s_ in range(4):
+            m = tg == s_
+            if m.any():
+                print(f"    CU slot (HW_ID tg_id) {s_}: {m.sum():4d} workgroups, end p50 {np.median(re_us[m]):.1f} us, "
+                      f"min {re_us[m].min():.1f} max {re_us[m].max():.1f}")
         lo = 4 if which == 2 else 0
         rows = []
         for i in range(SEGS):
