@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 
 #include "ddc_frame_common.hpp"
+#include "ddc_queue.hpp"
 
 namespace sddc {
 namespace {
@@ -491,46 +492,6 @@ __device__ __forceinline__ void emit_frame_q(void *__restrict__ out, int fbase, 
 }
 
 
-// Dynamic frame distribution.  With a static split (each workgroup a fixed contiguous range)
-// the four workgroups of a CU finish far apart: the SIMDs arbitrate by age, so the first-
-// dispatched workgroup of a CU runs ~1.6x faster than the last, and the CU spends the last
-// ~40 % of the launch with 3, 2, then 1 workgroup resident (s_memtime / s_memrealtime stamps
-// by HW_ID slot, profiles/r03/stamps).  Frames are handed out one at a time instead: 8 shards
-// of consecutive frames (one counter each, on its own 64-B line; a workgroup starts on shard
-// blockIdx % 8 and moves on when it runs dry), so consecutive frames, which share 2048 input
-// samples, mostly stay in one XCD's L2.  Thread 0 takes a ticket for the next frame at the start
-// of the current one and looks at it only before inverse pass 0's stores (the answer is needed
-// at inverse pass 1, for the next frame's input prefetch): waiting for the atomic where it is
-// issued cost wave 0 ~1800 cycles per frame (profiles/r03/stamps/stamps_q.txt).
-// wq: this launch's slot of the handle's queue ring, zero at entry; the last workgroup to leave
-// clears it for the slot's next launch (the counters are touched only by device-scope atomics).
-constexpr int FS_SHARDS = 8;
-static_assert(kFsQueueWords == 16 * (FS_SHARDS + 1), "queue slot: one 64-B line per shard counter + the done count");
-__device__ __forceinline__ int fs_shard_lo(int nframes, int s) { return (int)(((long long)nframes * s) / FS_SHARDS); }
-// the ticket of shard (sh0 + shn) mod 8; its value is looked at only by fs_resolve, so the wave
-// does not wait for the atomic where it is issued
-__device__ __forceinline__ unsigned fs_ticket(unsigned *wq, int sh0, int shn)
-{
-    return shn < FS_SHARDS ? atomicAdd(wq + 16 * ((sh0 + shn) & (FS_SHARDS - 1)), 1u) : 0u;
-}
-// the frame of a ticket, or (its shard run dry) the next shards' tickets in turn; -1 when all are
-__device__ __forceinline__ int fs_resolve(unsigned *wq, int nframes, int sh0, int &shn, unsigned ticket)
-{
-    while (shn < FS_SHARDS) {
-        const int s = (sh0 + shn) & (FS_SHARDS - 1);
-        const int lo = fs_shard_lo(nframes, s), hi = fs_shard_lo(nframes, s + 1);
-        if ((int)ticket < hi - lo) return lo + (int)ticket;
-        if (++shn < FS_SHARDS) ticket = fs_ticket(wq, sh0, shn);
-    }
-    return -1;
-}
-__device__ __forceinline__ void fs_queue_done(unsigned *wq, unsigned grid)
-{
-    if (atomicAdd(wq + 16 * FS_SHARDS, 1u) == grid - 1) {
-        for (int s = 0; s <= FS_SHARDS; s++) atomicExch(wq + 16 * s, 0u);
-    }
-}
-
 // Diagnostic build (-DSDDC_STAMPS, tools/fs_stamps.py; never the product): per wave, the cycles
 // (s_memtime) of each work segment between two barriers and of each barrier wait, summed over
 // the workgroup's frames in SGPRs, and written once at the end by lane 0 (vector stores) to a
@@ -545,8 +506,9 @@ constexpr int kFsStampWords = 2 * kFsSegs + 7;
 #ifdef SDDC_STAMPS
 // SDDC_STAMPS = 1 stamps barriers 0..3, = 2 barriers 4..7 (all eight in one build spill: the
 // accumulators live in SGPRs); the time of an unstamped barrier falls into the next work segment.
+// = 3: as 2, and the queue wave's dequeue in work[0..2]: resolve, the s_next write, the next ticket.
 __device__ unsigned g_fs_stamps[2048 * 4 * kFsStampWords];
-constexpr int kStLo = SDDC_STAMPS == 2 ? 4 : 0;
+constexpr int kStLo = SDDC_STAMPS >= 2 ? 4 : 0;
 #define FS_STAMP_INIT()                                                                              \
     unsigned st_work[kFsSegs] = {}, st_wait[kFsSegs] = {}, st_frames = 0;                          \
     unsigned long long st_t = __builtin_amdgcn_s_memtime(), st_a = st_t;                          \
@@ -570,6 +532,16 @@ constexpr int kStLo = SDDC_STAMPS == 2 ? 4 : 0;
         st_t = st_a;                                                                                 \
         st_frames++;                                                                                 \
     } while (0)
+#define FS_QSTAMP(i, x)                                                                              \
+    do {                                                                                             \
+        if constexpr (SDDC_STAMPS == 3) {                                                            \
+            const unsigned long long q0 = __builtin_amdgcn_s_memtime();                              \
+            x;                                                                                       \
+            st_work[i] += (unsigned)(__builtin_amdgcn_s_memtime() - q0);                             \
+        } else {                                                                                     \
+            x;                                                                                       \
+        }                                                                                            \
+    } while (0)
 #define FS_STAMP_WRITE(wg, tid, nfr)                                                                 \
     do {                                                                                             \
         const unsigned long long st_r1 = __builtin_amdgcn_s_memrealtime();                          \
@@ -592,6 +564,7 @@ constexpr int kStLo = SDDC_STAMPS == 2 ? 4 : 0;
 #define FS_STAMP_INIT() (void)0
 #define FS_SYNC(i) __syncthreads()
 #define FS_STAMP_FRAME_END() (void)0
+#define FS_QSTAMP(i, x) x
 #define FS_STAMP_WRITE(wg, tid, nfr) (void)0
 #endif
 
@@ -613,13 +586,30 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
     __shared__ __attribute__((aligned(16))) float2 wtab[2 * NT];
     __shared__ __attribute__((aligned(16))) float2 gtab[NT];
 
-    __shared__ int s_next;   // the workgroup's next frame (thread 0's dequeue), -1 when none is left
+    __shared__ int s_next;   // the workgroup's next frame (the queue wave's dequeue), -1 when none is left
 
     const int tid = (int)threadIdx.x;
     const int w = (int)blockIdx.x;
-    const int sh0 = w & (FS_SHARDS - 1);   // home shard (blockIdx % 8: the XCD under round-robin placement)
-    int shn = 0;                           // thread 0: shards found empty so far
-    if (tid == 0) s_next = fs_resolve(wq, nframes, sh0, shn, fs_ticket(wq, sh0, shn));
+    // the dynamic frame queue (ddc_queue.hpp), worked by wave SDDC_FS_QWAVE: a ticket is
+    // resolved a frame after it was taken (the frame after the current one is known at its
+    // inverse pass 0, for the prefetch; the one after that is in flight)
+#ifndef SDDC_FS_QWAVE
+#define SDDC_FS_QWAVE 3   // not wave 0, which also carries the self-mirrored columns' split
+#endif
+    constexpr int QLANE = 64 * SDDC_FS_QWAVE;
+    const bool qw = __builtin_amdgcn_readfirstlane(tid >> 6) == SDDC_FS_QWAVE;
+    FsQueue q;
+    q.init(wq, nframes, w & (FS_SHARDS - 1));   // home shard: blockIdx % 8, the XCD under round-robin placement
+    if (qw) {
+#ifdef SDDC_FS_QSTATIC
+        const int f_first = w < nframes ? w : -1;
+#else
+        q.take();
+        const int f_first = q.resolve();
+        q.take();
+#endif
+        if (tid == QLANE) s_next = f_first;
+    }
 
     // per-lane constants: the column, and (reloaded every frame from L2, to keep them out of
     // the registers of the other passes) the twiddle bases of the two NS = 256 passes
@@ -643,6 +633,9 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
     FS_STAMP_INIT();
 
     while (f >= 0) {
+#ifdef SDDC_FS_QEARLY
+        if (qw) FS_QSTAMP(3, q.peek());
+#endif
         int z = 0;
         asm volatile("" : "+s"(z));
         const int t = tid + z;
@@ -665,9 +658,6 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
                 }
             dft16<-1>(a, v);
         }
-        // thread 0 asks for the frame after this one now; the answer is needed by inverse pass 1
-        unsigned nq = 0;
-        if (tid == 0) nq = fs_ticket(wq, sh0, shn);
         FS_SYNC(0);   // the previous frame's last LDS reads are done
 #pragma unroll
         for (int r = 0; r < 16; r++) lds[16 * t + (r ^ x15)] = v[r];
@@ -760,7 +750,31 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
 #pragma unroll
             for (int r = 0; r < 16; r++) st_row(lds, xc0, r, 0, u[r]);
         }
-        if (tid == 0) s_next = fs_resolve(wq, nframes, sh0, shn, nq);
+        // the next frame from the ticket taken a frame ago, then a ticket for the one after it:
+        // taken after the resolve, so that the resolve's wait (the compiler cannot count the
+        // loop-carried atomic and waits for every older vector-memory operation) finds no young
+        // atomic in flight
+        if (qw) {
+#ifdef SDDC_FS_QSTATIC   // timing only: a static stride instead of the queue
+            FS_QSTAMP(1, {
+                if (tid == QLANE) s_next = f + (int)gridDim.x < nframes ? f + (int)gridDim.x : -1;
+            });
+#else
+            int f_n;
+#ifdef SDDC_FS_QPRIO   // timing experiment: the queue wave's dequeue at raised issue priority
+            __builtin_amdgcn_s_setprio(SDDC_FS_QPRIO);
+#endif
+#if defined(SDDC_STAMPS) && SDDC_STAMPS == 3 && defined(SDDC_FS_QWAIT) && !defined(SDDC_FS_QEARLY)
+            FS_QSTAMP(3, asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"));
+#endif
+            FS_QSTAMP(0, f_n = q.resolve());
+            FS_QSTAMP(1, if (tid == QLANE) s_next = f_n);
+            FS_QSTAMP(2, q.take());
+#ifdef SDDC_FS_QPRIO
+            __builtin_amdgcn_s_setprio(0);
+#endif
+#endif
+        }
         FS_SYNC(5);
         // the next frame's input: issued here rather than in pass 0, so its 16 registers are
         // free through forward pass 2 and the split, and the loads' waits never hold pass 2
@@ -814,7 +828,9 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
         f = fn;
     }
     FS_STAMP_WRITE(w, tid, st_frames);
-    if (tid == 0) fs_queue_done(wq, (unsigned)gridDim.x);
+#ifndef SDDC_FS_QSTATIC
+    if (tid == QLANE) fs_queue_done(wq, (unsigned)gridDim.x);
+#endif
 }
 
 // FS tables of one tunebin: pqf[l + 256 k] = (P, Q) of bin b = kFsPerm[l] + 256 k (inverse input

@@ -1,0 +1,102 @@
+// ddc_queue.hpp — dynamic frame distribution for the persistent single-channel kernels
+// (ddc_persistent.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+namespace sddc {
+namespace {
+
+// Dynamic frame distribution.  With a static split (each workgroup a fixed contiguous range)
+// the four workgroups of a CU finish far apart: the SIMDs arbitrate by age, so the first-
+// dispatched workgroup of a CU runs ~1.6x faster than the last, and the CU spends the last
+// ~40 % of the launch with 3, 2, then 1 workgroup resident (s_memtime / s_memrealtime stamps
+// by HW_ID slot, profiles/r03/stamps).  Frames are handed out one at a time instead: 8 shards
+// of consecutive frames (one counter each, on its own 64-B line; a workgroup starts on shard
+// blockIdx % 8 and moves on when it runs dry), so consecutive frames, which share 2048 input
+// samples, mostly stay in one XCD's L2.  Thread 0 resolves a ticket a frame after taking it,
+// before inverse pass 0's stores (the frame is needed at inverse pass 1, for its input prefetch),
+// and takes the next ticket right after.  A device-scope atomic's value is waited for with
+// vmcnt, in issue order with every other vector-memory operation of the wave; waiting for it in
+// the frame it was taken cost wave 0 ~1800 cycles per frame at pass 0, and taking the next
+// ticket before the resolve (which the compiler, unable to count the loop-carried atomic, turns
+// into a wait for everything outstanding) ~700 at inverse pass 0
+// (profiles/r03/stamps/stamps_q.txt, stamps_q2.txt, stamps_q3.txt).
+// wq: this launch's slot of the handle's queue ring, zero at entry; the last workgroup to leave
+// clears it for the slot's next launch (the counters are touched only by device-scope atomics).
+constexpr int FS_SHARDS = 8;
+static_assert(kFsQueueWords == 16 * (FS_SHARDS + 1), "queue slot: one 64-B line per shard counter + the done count");
+// first frame of shard s (32-bit: nframes * 8 < 2^31 for any batch the C ABI accepts)
+__device__ __forceinline__ int fs_shard_lo(int nframes, int s) { return (nframes * s) >> 3; }
+
+// The queue is worked by one wave (wave-uniform, so the bookkeeping is scalar); only the atomic
+// increment is its lane 0's.  Every wave instruction costs ~20 cycles of wall time at 4 waves per
+// SIMD, and the other waves wait for this one at the next barrier, so the per-frame path is a
+// handful of instructions: the ticket taken a frame earlier is read from lane 0
+// (v_readfirstlane), compared with the current shard's size, and the next one is taken.  The
+// whole wave issues the ticket's atomic as a buffer atomic whose lanes other than 0 fall outside
+// the buffer's range (dropped, no memory access): issued from a lane-0 branch instead, the
+// ticket register became a merge of two values and the merge copy waited for the atomic's
+// return right there, a device-scope round trip (~1200 cycles of the queue wave per frame at
+// inverse pass 0, profiles/r03/stamps/stamps_q8.txt).
+constexpr unsigned FS_OOB = 0x80000000u;   // a buffer offset past the queue slot's range
+struct FsQueue {
+    __amdgpu_buffer_rsrc_t rq;   // the queue slot as a buffer (kFsQueueWords words)
+    unsigned lane_oob;           // 0 on lane 0, FS_OOB elsewhere
+    int nframes, sh0;
+    int shn;        // shard of the pending ticket (8: every shard dry)
+    int lo, cnt;    // first frame and size of shard (sh0 + shn) mod 8
+    int tk;         // lane 0: the pending ticket
+
+    __device__ __forceinline__ void init(unsigned *wq, int nframes_, int home)
+    {
+        rq = __builtin_amdgcn_make_buffer_rsrc(wq, (short)0, 4 * kFsQueueWords, 0x00020000);
+        lane_oob = (threadIdx.x & 63) == 0 ? 0u : FS_OOB;
+        nframes = nframes_;
+        sh0 = home;
+        set_shard(0);
+    }
+    __device__ __forceinline__ void set_shard(int sh)
+    {
+        shn = sh;
+        const int s = (sh0 + sh) & (FS_SHARDS - 1);
+        lo = fs_shard_lo(nframes, s);
+        cnt = fs_shard_lo(nframes, s + 1) - lo;
+    }
+    // takes a ticket of the current shard (lane 0; no wait).  Called by the whole wave.
+    __device__ __forceinline__ void take()
+    {
+        const unsigned off = shn < FS_SHARDS ? 64u * (unsigned)((sh0 + shn) & (FS_SHARDS - 1)) : FS_OOB;
+        tk = __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(1, rq, lane_oob | off, 0, 0);
+    }
+    // the frame of the pending ticket; a ticket past its shard's end moves on to the next shard
+    // and takes (and waits for) a new ticket there: this happens only as the queue runs out.
+    // -1 when every shard is dry.
+    int pv;         // SDDC_FS_QEARLY (timing experiment): the pending ticket, read early
+    __device__ __forceinline__ void peek() { pv = __builtin_amdgcn_readfirstlane(tk); }
+    __device__ __forceinline__ int resolve()
+    {
+#ifdef SDDC_FS_QEARLY
+        int v = pv;
+#else
+        int v = __builtin_amdgcn_readfirstlane(tk);
+#endif
+        bool ok = shn < FS_SHARDS && v < cnt;
+        while (!ok && shn < FS_SHARDS) {   // rare: the shard ran dry
+            set_shard(shn + 1);
+            take();
+            v = __builtin_amdgcn_readfirstlane(tk);
+            ok = shn < FS_SHARDS && v < cnt;
+        }
+        return ok ? lo + v : -1;
+    }
+};
+__device__ __forceinline__ void fs_queue_done(unsigned *wq, unsigned grid)
+{
+    if (atomicAdd(wq + 16 * FS_SHARDS, 1u) == grid - 1) {
+        for (int s = 0; s <= FS_SHARDS; s++) atomicExch(wq + 16 * s, 0u);
+    }
+}
+
+}  // namespace
+}  // namespace sddc

@@ -1,0 +1,87 @@
+"""The float32 parity floor, measured (pytest -m gpu).
+
+north_star asks for IQ "within 1e-5 of the FFTW reference".  The reference's own path is float32
+(FFTW single precision), and on the adversarial "oob" input (a strong out-of-band tone, a weak
+in-band one) every float32 implementation sits close to 1e-5 of the exact answer: the oracle's
+float32 port of the reference algorithm (oracle/ddc_oracle.c, _f32), the library's AVX2 CPU
+backend and the HIP kernels each land at 5e-6 .. 9e-6 of the f64 oracle at d = 3, 4, and two such
+float32 paths can differ from each other by more than 1e-5 ("The float32 floor").
+So the bar the tests hold is against the exact (f64) answer, and this test records, per case,
+three numbers: HIP vs f64, port vs f64 and HIP vs port; it asserts that the HIP path is within
+1e-5 of exact and, where the port itself sits near the floor (>= 2e-6: the d = 3, 4 cases), at
+the float32 floor (<= 1.2 x the port's own error).  Far below the floor (d = 0: ~4e-7) the
+operation orders differ (the fused split modulates the output instead of shifting bins) and the
+bar is a tenth of the tolerance instead.  With SDDC_PARITY_RECORD set, the numbers are appended to
+that JSON-lines file.
+"""
+from __future__ import annotations
+
+import json
+import os
+
+import numpy as np
+import pytest
+
+from extio_sddc_amd.synth import make_stream
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-5
+FLOOR_FACTOR = 1.2
+AT_FLOOR = 2e-6     # the port's own error from which the floor comparison applies
+
+CASES = [
+    # d, tunebin, lsb, rand: the BASELINE C3 configs' out-of-band cases at d = 3, 4 (and d = 4 at
+    # tune bin 0 with the sideband inverted, the worst one the verdict measured)
+    (3, 1024, 0, 0),
+    (4, 1024, 0, 0),
+    (4, 0, 1, 0),
+    (0, 1024, 0, 0),
+]
+
+
+def _record(row):
+    path = os.environ.get("SDDC_PARITY_RECORD")
+    if path:
+        os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+        with open(path, "a") as f:
+            f.write(json.dumps(row) + "\n")
+
+
+@pytest.mark.parametrize("d,tb,lsb,rand", CASES)
+def test_float32_floor(oracle, d, tb, lsb, rand):
+    import torch
+    from extio_sddc_amd import DEVICE_CPU, R2iq, output_samples
+    assert torch.cuda.is_available(), "gpu tests need a GPU"
+    nblk = 4
+    x = make_stream(nblk, "oob")
+    H64, H32 = oracle.filter_bank(1.0), oracle.filter_bank(1.0, np.float32)
+    exact = oracle.r2iq(x, nblk, d, tb, lsb, rand, H=H64)
+    port = oracle.r2iq(x, nblk, d, tb, lsb, rand, dtype=np.float32, H=H32)
+    with R2iq(gain=1.0, device=0) as r:
+        r.setDecimate(d)
+        r.setTuneBin(tb)
+        r.setSideband(bool(lsb))
+        r.updateRand(bool(rand))
+        d_in = torch.from_numpy(x).to("cuda")
+        out = torch.full((output_samples(d, nblk) * 2,), float("nan"), dtype=torch.float32, device="cuda")
+        r.process_device(d_in, nblk, out)
+        torch.cuda.synchronize()
+        hip = out.cpu().numpy().view(np.complex64)
+    with R2iq(gain=1.0, device=DEVICE_CPU) as c:
+        c.setDecimate(d)
+        c.setTuneBin(tb)
+        c.setSideband(bool(lsb))
+        c.updateRand(bool(rand))
+        cpu = c.process(np.ascontiguousarray(x[4096:4096 + nblk * 65536]))
+    e = oracle.max_rel_err
+    row = {"d": d, "tunebin": tb, "lsb": lsb, "rand": rand, "source": "oob",
+           "hip_vs_f64": e(hip, exact), "port_f32_vs_f64": e(port, exact), "hip_vs_port_f32": e(hip, port),
+           "cpu_backend_vs_f64": e(cpu, exact), "cpu_backend_vs_port_f32": e(cpu, port)}
+    _record(row)
+    print(json.dumps(row))
+    assert row["hip_vs_f64"] <= TOL, row
+    if row["port_f32_vs_f64"] >= AT_FLOOR:
+        assert row["hip_vs_f64"] <= FLOOR_FACTOR * row["port_f32_vs_f64"], row
+    else:
+        assert row["hip_vs_f64"] <= 0.1 * TOL, row

@@ -101,7 +101,11 @@ def main():
             if m.any():
                 print(f"    CU slot (HW_ID tg_id) {s_}: {m.sum():4d} workgroups, end p50 {np.median(re_us[m]):.1f} us, "
                       f"min {re_us[m].min():.1f} max {re_us[m].max():.1f}")
-        lo = 4 if which == 2 else 0
+        lo = 4 if which >= 2 else 0
+        if which == 3:
+            for i, what in enumerate(("resolve", "s_next write", "next ticket", "QWAIT: vmcnt(0) lgkmcnt(0); QEARLY: early peek")):
+                qwk = [np.mean(st[:, w, i][ok[:, w]] / fr[:, w][ok[:, w]]) for w in range(4)]
+                print(f"  queue wave, inside seg 5: {what:36s} work " + " ".join(f"{x:7.0f}" for x in qwk))
         rows = []
         for i in range(SEGS):
             stamped = (lo <= i < lo + 4) or i == SEGS - 1
