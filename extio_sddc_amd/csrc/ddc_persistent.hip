@@ -506,7 +506,8 @@ constexpr int kFsStampWords = 2 * kFsSegs + 7;
 #ifdef SDDC_STAMPS
 // SDDC_STAMPS = 1 stamps barriers 0..3, = 2 barriers 4..7 (all eight in one build spill: the
 // accumulators live in SGPRs); the time of an unstamped barrier falls into the next work segment.
-// = 3: as 2, and the queue wave's dequeue in work[0..2]: resolve, the s_next write, the next ticket.
+// = 3: as 2, and the queue wave's dequeue in work[0..3]: resolve, the s_next write, the next ticket,
+// and the ticket's read at the frame top.
 __device__ unsigned g_fs_stamps[2048 * 4 * kFsStampWords];
 constexpr int kStLo = SDDC_STAMPS >= 2 ? 4 : 0;
 #define FS_STAMP_INIT()                                                                              \
@@ -605,6 +606,7 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
         const int f_first = w < nframes ? w : -1;
 #else
         q.take();
+        q.peek();
         const int f_first = q.resolve();
         q.take();
 #endif
@@ -633,9 +635,7 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
     FS_STAMP_INIT();
 
     while (f >= 0) {
-#ifdef SDDC_FS_QEARLY
         if (qw) FS_QSTAMP(3, q.peek());
-#endif
         int z = 0;
         asm volatile("" : "+s"(z));
         const int t = tid + z;
@@ -750,10 +750,8 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
 #pragma unroll
             for (int r = 0; r < 16; r++) st_row(lds, xc0, r, 0, u[r]);
         }
-        // the next frame from the ticket taken a frame ago, then a ticket for the one after it:
-        // taken after the resolve, so that the resolve's wait (the compiler cannot count the
-        // loop-carried atomic and waits for every older vector-memory operation) finds no young
-        // atomic in flight
+        // the next frame from the ticket read at this frame's top, then a ticket for the one after
+        // it (ddc_queue.hpp)
         if (qw) {
 #ifdef SDDC_FS_QSTATIC   // timing only: a static stride instead of the queue
             FS_QSTAMP(1, {
@@ -761,18 +759,9 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
             });
 #else
             int f_n;
-#ifdef SDDC_FS_QPRIO   // timing experiment: the queue wave's dequeue at raised issue priority
-            __builtin_amdgcn_s_setprio(SDDC_FS_QPRIO);
-#endif
-#if defined(SDDC_STAMPS) && SDDC_STAMPS == 3 && defined(SDDC_FS_QWAIT) && !defined(SDDC_FS_QEARLY)
-            FS_QSTAMP(3, asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"));
-#endif
             FS_QSTAMP(0, f_n = q.resolve());
             FS_QSTAMP(1, if (tid == QLANE) s_next = f_n);
             FS_QSTAMP(2, q.take());
-#ifdef SDDC_FS_QPRIO
-            __builtin_amdgcn_s_setprio(0);
-#endif
 #endif
         }
         FS_SYNC(5);

@@ -14,14 +14,14 @@ namespace {
 // by HW_ID slot, profiles/r03/stamps).  Frames are handed out one at a time instead: 8 shards
 // of consecutive frames (one counter each, on its own 64-B line; a workgroup starts on shard
 // blockIdx % 8 and moves on when it runs dry), so consecutive frames, which share 2048 input
-// samples, mostly stay in one XCD's L2.  Thread 0 resolves a ticket a frame after taking it,
-// before inverse pass 0's stores (the frame is needed at inverse pass 1, for its input prefetch),
-// and takes the next ticket right after.  A device-scope atomic's value is waited for with
-// vmcnt, in issue order with every other vector-memory operation of the wave; waiting for it in
-// the frame it was taken cost wave 0 ~1800 cycles per frame at pass 0, and taking the next
-// ticket before the resolve (which the compiler, unable to count the loop-carried atomic, turns
-// into a wait for everything outstanding) ~700 at inverse pass 0
-// (profiles/r03/stamps/stamps_q.txt, stamps_q2.txt, stamps_q3.txt).
+// samples, mostly stay in one XCD's L2.  The queue wave (SDDC_FS_QWAVE) reads a ticket at the
+// top of the frame after the one it was taken in, resolves it before inverse pass 1 (the frame
+// is needed there, for its input prefetch) and takes the next ticket right after.  A device-
+// scope atomic's value is waited for with vmcnt, in issue order with every other vector-memory
+// operation of the wave; waiting for it in the frame it was taken cost ~1800 cycles per frame
+// (profiles/r03/stamps/stamps_q.txt .. stamps_q18.txt trace the variants; A/B in profiles/r03/ab).
+// The queue's remaining cost is ~700 cycles of the queue wave per frame at inverse pass 0 (the
+// other waves wait for it at the next barrier), against the ~8 % the static split lost.
 // wq: this launch's slot of the handle's queue ring, zero at entry; the last workgroup to leave
 // clears it for the slot's next launch (the counters are touched only by device-scope atomics).
 constexpr int FS_SHARDS = 8;
@@ -43,10 +43,12 @@ constexpr unsigned FS_OOB = 0x80000000u;   // a buffer offset past the queue slo
 struct FsQueue {
     __amdgpu_buffer_rsrc_t rq;   // the queue slot as a buffer (kFsQueueWords words)
     unsigned lane_oob;           // 0 on lane 0, FS_OOB elsewhere
+    unsigned voff;               // the ticket atomic's offset: lane 0 the current shard's counter
     int nframes, sh0;
     int shn;        // shard of the pending ticket (8: every shard dry)
-    int lo, cnt;    // first frame and size of shard (sh0 + shn) mod 8
+    int lo, cnt;    // first frame and size of that shard (cnt = 0 once every shard is dry)
     int tk;         // lane 0: the pending ticket
+    int pv;         // its value, read by peek()
 
     __device__ __forceinline__ void init(unsigned *wq, int nframes_, int home)
     {
@@ -61,34 +63,29 @@ struct FsQueue {
         shn = sh;
         const int s = (sh0 + sh) & (FS_SHARDS - 1);
         lo = fs_shard_lo(nframes, s);
-        cnt = fs_shard_lo(nframes, s + 1) - lo;
+        cnt = sh < FS_SHARDS ? fs_shard_lo(nframes, s + 1) - lo : 0;
+        voff = sh < FS_SHARDS ? lane_oob | (64u * (unsigned)s) : FS_OOB;
     }
     // takes a ticket of the current shard (lane 0; no wait).  Called by the whole wave.
-    __device__ __forceinline__ void take()
-    {
-        const unsigned off = shn < FS_SHARDS ? 64u * (unsigned)((sh0 + shn) & (FS_SHARDS - 1)) : FS_OOB;
-        tk = __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(1, rq, lane_oob | off, 0, 0);
-    }
-    // the frame of the pending ticket; a ticket past its shard's end moves on to the next shard
+    __device__ __forceinline__ void take() { tk = __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(1, rq, voff, 0, 0); }
+    // reads the pending ticket (waits for its atomic): at the top of a frame, where the wait is
+    // free (the atomic is older than the frame's input loads, which are needed there anyway) and
+    // nothing reads the result soon (v_readfirstlane's SGPR feeding a scalar compare right away
+    // stalled the queue wave ~500 cycles per frame at inverse pass 0, stamps_q15.txt)
+    __device__ __forceinline__ void peek() { pv = __builtin_amdgcn_readfirstlane(tk); }
+    // the frame of the peeked ticket; a ticket past its shard's end moves on to the next shard
     // and takes (and waits for) a new ticket there: this happens only as the queue runs out.
     // -1 when every shard is dry.
-    int pv;         // SDDC_FS_QEARLY (timing experiment): the pending ticket, read early
-    __device__ __forceinline__ void peek() { pv = __builtin_amdgcn_readfirstlane(tk); }
     __device__ __forceinline__ int resolve()
     {
-#ifdef SDDC_FS_QEARLY
-        int v = pv;
-#else
-        int v = __builtin_amdgcn_readfirstlane(tk);
-#endif
-        bool ok = shn < FS_SHARDS && v < cnt;
-        while (!ok && shn < FS_SHARDS) {   // rare: the shard ran dry
+        bool dry = pv >= cnt;
+        while (__builtin_expect(dry && shn < FS_SHARDS, 0)) {
             set_shard(shn + 1);
             take();
-            v = __builtin_amdgcn_readfirstlane(tk);
-            ok = shn < FS_SHARDS && v < cnt;
+            pv = __builtin_amdgcn_readfirstlane(tk);
+            dry = pv >= cnt;
         }
-        return ok ? lo + v : -1;
+        return dry ? -1 : lo + pv;
     }
 };
 __device__ __forceinline__ void fs_queue_done(unsigned *wq, unsigned grid)

@@ -103,7 +103,7 @@ def main():
                       f"min {re_us[m].min():.1f} max {re_us[m].max():.1f}")
         lo = 4 if which >= 2 else 0
         if which == 3:
-            for i, what in enumerate(("resolve", "s_next write", "next ticket", "QWAIT: vmcnt(0) lgkmcnt(0); QEARLY: early peek")):
+            for i, what in enumerate(("resolve", "s_next write", "next ticket", "ticket read (frame top)")):
                 qwk = [np.mean(st[:, w, i][ok[:, w]] / fr[:, w][ok[:, w]]) for w in range(4)]
                 print(f"  queue wave, inside seg 5: {what:36s} work " + " ".join(f"{x:7.0f}" for x in qwk))
         rows = []
