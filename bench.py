@@ -254,6 +254,7 @@ VALU_SIMDS = 1024
 VALU_CYCLES_PER_INST = 2.0
 CLOCK_HZ = 2.4e9
 VALU_PEAK_INST_PER_S = VALU_SIMDS * CLOCK_HZ / VALU_CYCLES_PER_INST
+FP32_PEAK = 157.3e12   # FLOP/s, vector FP32 at 2.4 GHz (MI355X_MICROARCH.md)
 
 
 def load_valu(workload: str):
@@ -268,19 +269,48 @@ def load_valu(workload: str):
 
 
 def compute_roofline(workload: str, kern_ms: float):
-    """The bound the d = 0 kernel actually sits on: VALU issue.  achieved =
-    counted VALU wave-instructions per launch / the launch's HIP-event time; peak = the chip's
-    wave-instruction issue rate.  None when the workload has no committed count."""
+    """The compute-side bounds of a launch, from the per-config counters of
+    profiles/pmc_valu.json (tools/gpu_pmc_configs.sh + tools/pmc_configs.py): VALU issue =
+    counted VALU wave-instructions per launch / this run's HIP-event time, against the chip's
+    wave-instruction issue rate at the 2.4 GHz maximum clock and at the effective clock the
+    counters' pass measured (GRBM_GUI_ACTIVE / 8 / dispatch time, MI355X_MICROARCH.md 'DVFS
+    give-back'); and, where counted, FP32 FLOP/s against the 157.3 TF vector peak, scaled the
+    same way.  None when the workload has no committed count."""
     v = load_valu(workload)
     if not v:
         return None
     n = float(v["valu_insts_per_launch"])
-    ach = n / (kern_ms * 1e-3)
-    return {"bound": "valu-issue", "achieved": ach, "peak": VALU_PEAK_INST_PER_S, "unit": "wave-instructions/s",
-            "frac": ach / VALU_PEAK_INST_PER_S, "valu_insts_per_launch": n,
-            "peak_basis": f"{VALU_SIMDS} SIMDs x {CLOCK_HZ / 1e9:.1f} GHz / {VALU_CYCLES_PER_INST:g} cycles per "
-                          "wave64 VALU instruction",
-            "source": v.get("source")}
+    t = kern_ms * 1e-3
+    ach = n / t
+    f_eff = v.get("effective_clock_hz")
+    out = {"bound": "valu-issue", "achieved": ach, "peak": VALU_PEAK_INST_PER_S, "unit": "wave-instructions/s",
+           "frac": ach / VALU_PEAK_INST_PER_S, "valu_insts_per_launch": n,
+           "peak_basis": f"{VALU_SIMDS} SIMDs x {CLOCK_HZ / 1e9:.1f} GHz / {VALU_CYCLES_PER_INST:g} cycles per "
+                         "wave64 VALU instruction",
+           "source": v.get("source")}
+    if f_eff:
+        peak_eff = VALU_SIMDS * f_eff / VALU_CYCLES_PER_INST
+        out.update({"effective_clock_hz": f_eff, "peak_at_effective_clock": peak_eff,
+                    "frac_at_effective_clock": ach / peak_eff})
+    if v.get("fp32_flops_per_launch"):
+        fl = float(v["fp32_flops_per_launch"])
+        out["fp32"] = {"flops_per_launch": fl, "achieved_tflops": fl / t / 1e12, "peak_tflops": FP32_PEAK / 1e12,
+                       "frac": fl / t / FP32_PEAK,
+                       "frac_at_effective_clock": fl / t / (FP32_PEAK * f_eff / CLOCK_HZ) if f_eff else None,
+                       "flop_per_algorithmic_byte": v.get("arithmetic_intensity_flop_per_byte"),
+                       "basis": "64 x (ADD_F32 + MUL_F32) + 128 x FMA_F32 wave-instructions (SQ_INSTS_VALU_*_F32)"}
+    if v.get("stalls"):
+        out["stalls"] = v["stalls"]
+    return out
+
+
+def sweep_counters(name: str, kern_ms: float) -> dict:
+    """traffic + compute of one sweep config (profiles/pmc_*.json keys = the config names)."""
+    key = "single d=0 nblk=2048" if name == "C3 decim 2" else name
+    t = load_traffic(key)
+    return {"traffic": t["hbm_bytes_per_launch"] if t else None,
+            "traffic_over_algorithmic": t.get("traffic_over_algorithmic") if t else None,
+            "compute": compute_roofline(key, kern_ms)}
 
 
 class ChannelRun:
@@ -426,6 +456,8 @@ def c5_leg(torch, dist, args, dev, stream, world: int, rank: int, backend: str) 
            "bytes_per_rank_per_batch": bytes_rank,
            "broadcast": info or ("none (one rank)" if world == 1 else None),
            "broadcast_check": ch.bcast_check}
+    if world == 1 and nblk5 == 256:   # the profiled launch (tools/gpu_pmc_configs.sh): one rank, all channels
+        out.update(sweep_counters("C5 1024 channels d=4 nblk=256", ms))
     del ch, ddc5
     torch.cuda.empty_cache()
     return out
@@ -592,9 +624,9 @@ def main() -> None:
             e1.record(stream)
             torch.cuda.synchronize()
             ms = e0.elapsed_time(e1) / 50
-            sweep.append({"config": name, "d": dd, "lsb": lsb, "rand": rnd, "gpu_input_MSps": nblk * BLOCK / ms / 1e3,
-                          "roofline_frac": nblk * BLOCK * algorithmic_bytes_per_sample(dd) / (ms * 1e-3) / 1e9
-                          / HBM_PEAK_GBS, "kernel_ms": ms})
+            sweep.append(dict({"config": name, "d": dd, "lsb": lsb, "rand": rnd, "gpu_input_MSps": nblk * BLOCK / ms / 1e3,
+                               "roofline_frac": nblk * BLOCK * algorithmic_bytes_per_sample(dd) / (ms * 1e-3) / 1e9
+                               / HBM_PEAK_GBS, "kernel_ms": ms}, **(sweep_counters(name, ms) if nblk == 2048 else {})))
         ddc.setDecimate(d)
         ddc.setSideband(False)
         ddc.updateRand(False)
@@ -625,7 +657,8 @@ def main() -> None:
                      "traffic": traffic["hbm_bytes_per_launch"] if traffic else None,
                      "traffic_unit": "bytes per launch (rocprofv3 FETCH_SIZE/WRITE_SIZE, calibrated)",
                      "traffic_detail": traffic,
-                     "kernel": "r2iq_persistent_kernel" if args.mode == "single" else "r2iq_channels_kernel",
+                     "kernel": ((traffic or {}).get("kernel") or ("r2iq_fs_kernel" if d == 0 else "r2iq_persistent_kernel"))
+                               if args.mode == "single" else "r2iq_channels_kernel",
                      "kernel_ms_per_launch": kern_ms,
                      "algorithmic_bytes_per_launch": alg_bytes,
                      "bytes_per_input_sample": algorithmic_bytes_per_sample(d, nch_local, out_bytes),
