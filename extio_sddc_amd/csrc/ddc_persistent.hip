@@ -105,7 +105,7 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
     const int *__restrict__ in32, void *__restrict__ out, int nframes,
     const float2 *__restrict__ tw_p1, const float2 *__restrict__ tw_q1,
     const float2 *__restrict__ rec_f, const float2 *__restrict__ rec_i, const float2 *__restrict__ tw4096,
-    const float4 *__restrict__ pq, int tunebin, OutArgs oa, NcoArgs nco)
+    const float4 *__restrict__ pq, int tunebin, OutArgs oa, NcoArgs nco, unsigned *__restrict__ wq)
 {
     constexpr int N = HALF >> D;
     // d >= 2 (N <= 1024): the inverse reads only the band [s0, s0 + N) of Z and its mirror
@@ -162,9 +162,42 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
 
     const int tid = (int)threadIdx.x;
     const int G = (int)gridDim.x, w = (int)blockIdx.x;
-    const int f0 = (int)(((long long)nframes * w) / G);
-    const int f1 = (int)(((long long)nframes * (w + 1)) / G);
-    if (f0 >= f1) return;
+    // d <= 2: frames come from the dynamic frame queue (ddc_queue.hpp), worked by wave 3: the frame
+    // after the next one is resolved in the middle of each frame (the next one's input is
+    // prefetched at the frame's start), from a ticket taken a frame earlier.  d = 1 +4 %, d = 2
+    // +1 %, but d = 3 -2 % and d = 4 -4 % (their inverse runs on one wave, and the queue's scalar
+    // state spills), so d >= 3 (and SDDC_P_QUEUE=0, timing only) keep the static contiguous split
+    // (profiles/r03/ab/pq_dynamic_queue_d1_4.txt).
+#ifndef SDDC_P_QUEUE
+#define SDDC_P_QUEUE 1
+#endif
+    constexpr bool PQ = SDDC_P_QUEUE && D <= 2;
+    __shared__ int s_first, s_next;
+    constexpr int QLANE = 64 * 3;
+    const bool qw = __builtin_amdgcn_readfirstlane(tid >> 6) == 3;
+    const int f1s = (int)(((long long)nframes * (w + 1)) / G);   // the static split's range end
+    FsQueue q;
+    if constexpr (PQ) q.init(wq, nframes, w & (FS_SHARDS - 1));
+    if (qw) {
+        int g0, g1;
+        if constexpr (PQ) {
+            q.take();
+            q.peek();
+            g0 = q.resolve();
+            q.take();
+            q.peek();
+            g1 = q.resolve();
+            q.take();
+        } else {
+            const int f0 = (int)(((long long)nframes * w) / G);
+            g0 = f0 < f1s ? f0 : -1;
+            g1 = f0 + 1 < f1s ? f0 + 1 : -1;
+        }
+        if (tid == QLANE) {
+            s_first = g0;
+            s_next = g1;
+        }
+    }
 
     // per-thread constants, live for the whole frame loop
     const int zr = ZROT ? (tunebin >> 8) + (tid < zd ? 1 : 0) : r0;
@@ -180,11 +213,14 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
     for (int i = tid; i < 15 * 16 + 15 * SQ; i += NT)
         twl[i] = i < 15 * 16 ? tw_p1[i] : tw_q1[i - 15 * 16];   // visible after the first frame's pass-0 barrier
 
-    int blk = f0 / FRAMES, k = f0 - blk * FRAMES;
+    __syncthreads();   // s_first, s_next
+    int f = s_first;
+    int blk = f / FRAMES, k = f - blk * FRAMES;
     int x[16];
-    load_frame(in32, blk, k, x);
+    if (f >= 0) load_frame(in32, blk, k, x);
 
-    for (int f = f0; f < f1; f++) {
+    while (f >= 0) {
+        const int fn = s_next;   // the next frame (written in the previous frame's middle)
         // Opaque per-iteration copies of the thread index and table pointers: without
         // them the compiler hoists every loop-invariant LDS address and table load out
         // of the frame loop and spills them.
@@ -219,11 +255,11 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
                 } else {
                     a[r] = make_float2((float)(int)(short)(x[r] & 0xffff), (float)(x[r] >> 16));
                 }
-            if (++k == FRAMES) {
-                k = 0;
-                ++blk;
+            if (fn >= 0) {   // prefetch the next frame
+                blk = fn / FRAMES;
+                k = fn - blk * FRAMES;
+                load_frame(in32, blk, k, x);
             }
-            if (f + 1 < f1) load_frame(in32, blk, k, x);   // prefetch the next frame
             dft16<-1>(a, v);
         }
         __syncthreads();   // the previous frame's last LDS reads are done
@@ -267,6 +303,16 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
             const int sZ = (t - zd) & 255;
 #pragma unroll
             for (int r = 0; r < 16; r++) w0[sZ + NT * r] = v[r];   // Z, rotated by tb
+        }
+        if (qw) {   // the frame after the next one (read by every wave at the next frame's start)
+            if constexpr (PQ) {
+                q.peek();
+                const int g = q.resolve();
+                if (tid == QLANE) s_next = g;
+                q.take();
+            } else if (tid == QLANE) {
+                s_next = fn >= 0 && fn + 1 < f1s ? fn + 1 : -1;
+            }
         }
         __syncthreads();
 
@@ -397,7 +443,10 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
                 emit_frame<NB, NCO, CS16>(out, oblk + emit_base<N>(kc), kc, t, u, oa, nco);
             }
         }
+        f = fn;
     }
+    if constexpr (PQ)
+        if (tid == QLANE) fs_queue_done(wq, (unsigned)G);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -887,6 +936,7 @@ struct Launch {
     hipStream_t s;
     OutArgs oa;
     NcoArgs nco;
+    unsigned *wq;   // a zeroed dynamic-frame-queue slot (kFsQueueWords)
 };
 
 template <int D, bool RAND, bool NCO, bool CS16>
@@ -901,7 +951,7 @@ hipError_t launch_v(const KernelTables &t, const Launch &L)
     if (grid > nframes) grid = nframes;
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), 0, L.s, reinterpret_cast<const int *>(L.d_in),
                        L.d_out, nframes, t.tw_p1, t.tw_q1[D], t.rec_f, t.rec_i[D], t.tw4096, L.pq, L.tunebin, L.oa,
-                       L.nco);
+                       L.nco, L.wq);
     return hipGetLastError();
 }
 
@@ -971,7 +1021,7 @@ hipError_t launch_frames_fs(const KernelTables &t, const int16_t *d_in, int nblk
 {
     if (tunebin & 3) return hipErrorInvalidValue;
     const Launch L{d_in, nblk, d_out, nullptr, tunebin, device, s, OutArgs{lsb ? 0x80000000u : 0u, cs16_scale},
-                   NcoArgs{nco_starts, nco_trig}};
+                   NcoArgs{nco_starts, nco_trig}, wq};
     const bool nco = nco_starts != nullptr;
     if (rand) {
         if (nco) return cs16 ? launch_fs_v<true, true, true>(t, L, pqf, fsl, wq) : launch_fs_v<true, true, false>(t, L, pqf, fsl, wq);
@@ -983,10 +1033,11 @@ hipError_t launch_frames_fs(const KernelTables &t, const int16_t *d_in, int nblk
 
 hipError_t launch_frames_persistent(const KernelTables &t, int d, const int16_t *d_in, int nblk, void *d_out,
                                     const float4 *pq, int tunebin, int lsb, int rand, int cs16, float cs16_scale,
-                                    const float2 *nco_starts, const float2 *nco_trig, int device, hipStream_t s)
+                                    const float2 *nco_starts, const float2 *nco_trig, unsigned *wq, int device,
+                                    hipStream_t s)
 {
     const Launch L{d_in, nblk, d_out, pq, tunebin, device, s, OutArgs{lsb ? 0x80000000u : 0u, cs16_scale},
-                   NcoArgs{nco_starts, nco_trig}};
+                   NcoArgs{nco_starts, nco_trig}, wq};
     const bool f = cs16 != 0;
     switch (d) {
     case 0: return launch_d<0>(t, L, rand, f);

@@ -42,8 +42,6 @@ __device__ __forceinline__ int fs_shard_lo(int nframes, int s) { return (nframes
 constexpr unsigned FS_OOB = 0x80000000u;   // a buffer offset past the queue slot's range
 struct FsQueue {
     __amdgpu_buffer_rsrc_t rq;   // the queue slot as a buffer (kFsQueueWords words)
-    unsigned lane_oob;           // 0 on lane 0, FS_OOB elsewhere
-    unsigned voff;               // the ticket atomic's offset: lane 0 the current shard's counter
     int nframes, sh0;
     int shn;        // shard of the pending ticket (8: every shard dry)
     int lo, cnt;    // first frame and size of that shard (cnt = 0 once every shard is dry)
@@ -53,7 +51,6 @@ struct FsQueue {
     __device__ __forceinline__ void init(unsigned *wq, int nframes_, int home)
     {
         rq = __builtin_amdgcn_make_buffer_rsrc(wq, (short)0, 4 * kFsQueueWords, 0x00020000);
-        lane_oob = (threadIdx.x & 63) == 0 ? 0u : FS_OOB;
         nframes = nframes_;
         sh0 = home;
         set_shard(0);
@@ -64,10 +61,16 @@ struct FsQueue {
         const int s = (sh0 + sh) & (FS_SHARDS - 1);
         lo = fs_shard_lo(nframes, s);
         cnt = sh < FS_SHARDS ? fs_shard_lo(nframes, s + 1) - lo : 0;
-        voff = sh < FS_SHARDS ? lane_oob | (64u * (unsigned)s) : FS_OOB;
     }
-    // takes a ticket of the current shard (lane 0; no wait).  Called by the whole wave.
-    __device__ __forceinline__ void take() { tk = __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(1, rq, voff, 0, 0); }
+    // takes a ticket of the current shard (lane 0; no wait).  Called by the whole wave; the
+    // offset is recomputed here (a few scalar instructions and one select) rather than kept in
+    // registers across the frame.
+    __device__ __forceinline__ void take()
+    {
+        const unsigned off = shn < FS_SHARDS ? 64u * (unsigned)((sh0 + shn) & (FS_SHARDS - 1)) : FS_OOB;
+        const unsigned voff = (threadIdx.x & 63) == 0 ? off : FS_OOB;
+        tk = __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(1, rq, voff, 0, 0);
+    }
     // reads the pending ticket (waits for its atomic): at the top of a frame, where the wait is
     // free (the atomic is older than the frame's input loads, which are needed there anyway) and
     // nothing reads the result soon (v_readfirstlane's SGPR feeding a scalar compare right away

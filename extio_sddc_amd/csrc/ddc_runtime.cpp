@@ -208,7 +208,7 @@ struct sddc_ddc {
     // the d = 0 fused-split kernel's per-tunebin tables: pqf (4096 float4) then fsl (768 float2)
     float4 *d_fs = nullptr;
     int fs_tb = -1;
-    // the fused-split kernel's dynamic frame queues: a ring of kQueueSlots zeroed slots, one per
+    // the single-channel kernels' dynamic frame queues: a ring of kQueueSlots zeroed slots, one per
     // launch in turn (each launch leaves its slot zeroed; the ring lets launches on different
     // streams overlap)
     static constexpr int kQueueSlots = 64;
@@ -578,6 +578,14 @@ static hipError_t stage_nco(sddc_ddc_t *h, int nblk, hipStream_t s)
     return hipEventRecord(h->nco_ev[slot], s);
 }
 
+// the next slot of the handle's dynamic-frame-queue ring (under h->mu, like every launch)
+static unsigned *next_queue_slot(sddc_ddc_t *h)
+{
+    unsigned *wq = h->d_queue + (size_t)h->queue_slot * sddc::kFsQueueWords;
+    h->queue_slot = (h->queue_slot + 1) % sddc_ddc::kQueueSlots;
+    return wq;
+}
+
 static hipError_t launch_single(sddc_ddc_t *h, const int16_t *d_in, int nblk, void *d_out, hipStream_t s)
 {
     const sddc_variants_api *V = h->variant ? variants() : nullptr;   // set_variant checked it loads
@@ -621,8 +629,7 @@ static hipError_t launch_single(sddc_ddc_t *h, const int16_t *d_in, int nblk, vo
             if (e != hipSuccess) return e;
             h->fs_tb = h->tunebin;
         }
-        unsigned *wq = h->d_queue + (size_t)h->queue_slot * sddc::kFsQueueWords;
-        h->queue_slot = (h->queue_slot + 1) % sddc_ddc::kQueueSlots;
+        unsigned *wq = next_queue_slot(h);
         hipError_t e = sddc::launch_frames_fs(h->tables, d_in, nblk, d_out, pqf, fsl, h->tunebin, h->lsb, h->rand,
                                               h->out_fmt == SDDC_DDC_FMT_CS16, h->cs16_scale, nco_starts, nco_trig,
                                               wq, h->device, s);
@@ -652,7 +659,7 @@ static hipError_t launch_single(sddc_ddc_t *h, const int16_t *d_in, int nblk, vo
                                         h->device, s)
         : sddc::launch_frames_persistent(h->tables, h->d, d_in, nblk, d_out, h->d_pq, h->tunebin, h->lsb, h->rand,
                                          h->out_fmt == SDDC_DDC_FMT_CS16, h->cs16_scale, nco_starts, nco_trig,
-                                         h->device, s);
+                                         next_queue_slot(h), h->device, s);
     if (e != hipSuccess) return e;
     return h->readers.record(s);
 }
