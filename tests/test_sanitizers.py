@@ -4,7 +4,12 @@ build/tsan/r2iq_harness (-fsanitize=thread), built by `make -C extio_sddc_amd/cs
 drive fft_mt_r2iq through r2iqControlClass on the CPU backend (SDDC_DDC_BACKEND=cpu): the
 worker and writer threads, both rings, the batch hand-off, per-block tune/rand changes and
 Start/Stop cycles, the C ABI front and the AVX2 r2iq.  Every run must be report-free and its
-IQ equal to the oracle's."""
+IQ equal to the oracle's.
+
+build/tsan/handles_harness (tests/harness/handles_harness.cpp) drives the C ABI from several
+threads at once, each with handles of its own plus one shared handle, on the CPU backend here
+and on device 0 in the GPU tier, where the kernel objects' host side (launch functions, the
+per-handle launch-geometry cache, the queue-slot ring) is instrumented too."""
 from __future__ import annotations
 
 import os
@@ -52,3 +57,31 @@ def test_dropin_threads_under_sanitizer(tmp_path, oracle, harnesses, kind, d, nb
     ref = oracle.r2iq(x, nblk, d, last[1], False, last[2])
     for c in range(1, cycles):
         assert oracle.max_rel_err(y[c], ref) <= 1e-5
+
+
+HANDLES = os.path.join(ROOT, "build", "tsan", "handles_harness")
+
+
+SUPP = os.path.join(ROOT, "tests", "harness", "tsan_hip.supp")
+
+
+def _run_handles(device: int, threads: int, iters: int):
+    # the HIP / HSA runtimes are uninstrumented: reports with a stack inside them are suppressed
+    # (tests/harness/tsan_hip.supp); races between this repository's own accesses still fail
+    p = subprocess.run([HANDLES, str(device), str(threads), str(iters)], capture_output=True, text=True,
+                       timeout=110, env=dict(os.environ, TSAN_OPTIONS=f"halt_on_error=0 suppressions={SUPP}"))
+    assert p.returncode == 0, p.stdout + p.stderr[-4000:]
+    for r in REPORTS:
+        assert r not in p.stderr, p.stderr[-4000:]
+    assert f"{threads} threads x {iters} iterations" in p.stdout and "0 failures" in p.stdout, p.stdout
+
+
+def test_handles_from_threads_tsan_cpu(harnesses):
+    _run_handles(-1, 4, 3)
+
+
+@pytest.mark.gpu
+def test_handles_from_threads_tsan_gpu():
+    # prebuilt in the build container (build() / make sanitize): a GPU box runs, never builds
+    assert os.path.exists(HANDLES), "build/tsan/handles_harness missing: make -C extio_sddc_amd/csrc sanitize"
+    _run_handles(0, 4, 3)
