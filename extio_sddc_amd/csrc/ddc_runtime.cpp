@@ -237,12 +237,21 @@ struct sddc_ddc {
     // fault injection for failover tests (GPU handles): environment SDDC_DDC_INJECT_FAIL=N
     // makes the (N+1)-th process_* call fail with SDDC_ERR_HIP before any device work
     long inject_fail = -1;
+    long inject_late = -1;   // SDDC_DDC_INJECT_FAIL_AFTER_D2H
 };
 
 static bool injected_failure(sddc_ddc_t *h)
 {
     if (h->inject_fail < 0) return false;
     return h->inject_fail-- == 0;
+}
+// SDDC_DDC_INJECT_FAIL_AFTER_D2H=N: the (N+1)-th host call fails after its first chunk's kernel and
+// D2H were issued, i.e. with device work in flight and the output partly written (a mid-stream
+// HIP error as the drop-in's failover meets it)
+static bool injected_late_failure(sddc_ddc_t *h)
+{
+    if (h->inject_late < 0) return false;
+    return h->inject_late-- == 0;
 }
 
 extern "C" {
@@ -328,6 +337,7 @@ int sddc_ddc_create(float gain, int device, sddc_ddc_t **out)
     h->device = device;
     h->gain = gain;
     if (const char *inj = std::getenv("SDDC_DDC_INJECT_FAIL")) h->inject_fail = std::atol(inj);
+    if (const char *inj = std::getenv("SDDC_DDC_INJECT_FAIL_AFTER_D2H")) h->inject_late = std::atol(inj);
 
     // ---- constant tables (one device allocation) ----
     auto W = [](double num, double den) {   // e^{-2 pi i num/den}, double -> float once
@@ -421,6 +431,10 @@ int sddc_ddc_destroy(sddc_ddc_t *h)
     {
         DeviceGuard g(h->device);
         if (h->stream) (void)hipStreamSynchronize(h->stream);
+        // copies a failed call left in flight (host_pipeline returns on the first error) finish
+        // before their buffers and registrations go
+        if (h->s_in) (void)hipStreamSynchronize(h->s_in);
+        if (h->s_out) (void)hipStreamSynchronize(h->s_out);
         // launches on the callers' streams may still read the tables below: wait for them first
         (void)h->readers.sync();
         (void)h->ch_readers.sync();
@@ -918,6 +932,8 @@ static int host_pipeline(sddc_ddc_t *h, int nblk, Src src, void *out)
             pend_off = (size_t)done * per_out;
         }
         HIP_TRY(hipEventRecord(sl.e_d2h, s_out));
+        if (done == 0 && injected_late_failure(h))
+            return fail(SDDC_ERR_HIP, "injected failure after the first chunk's D2H (SDDC_DDC_INJECT_FAIL_AFTER_D2H)");
     }
     if (int rc = drain()) return rc;
     HIP_TRY(hipStreamSynchronize(s_out));

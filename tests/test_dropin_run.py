@@ -173,6 +173,30 @@ def test_dropin_auto_failover_mid_stream(tmp_path, oracle, d, nblk, fail_after, 
         assert oracle.max_rel_err(y[a * per: b * per], ref) <= TOL, (a, b)
 
 
+@pytest.mark.gpu
+def test_dropin_auto_failover_with_device_work_in_flight(tmp_path, oracle):
+    """As above, but the failing call errors after its first chunk's kernel and D2H were issued
+    (SDDC_DDC_INJECT_FAIL_AFTER_D2H): the output stage is partly written and device work is in
+    flight when the worker destroys the failed GPU handle (which must neither block nor abort)
+    and redoes the batch on the CPU, overwriting the stage.  The stream stays continuous."""
+    d, tb, nblk = 1, 1228, 12
+    sched = [(4, 1228, 1), (8, 1228, 0)]
+    x = make_stream(nblk, "mix")
+    fin, fout = tmp_path / "in.bin", tmp_path / "out.bin"
+    x[4096:].tofile(fin)
+    spec = ",".join(f"{k}:{t}:{r}" for k, t, r in sched)
+    out, err = _run([HARNESS, str(fin), str(nblk), str(d), str(tb), "0", "0", "1.0", str(fout)], "auto",
+                    env={"SDDC_DDC_INJECT_FAIL_AFTER_D2H": "1", "R2IQ_SCHEDULE": spec}, stderr=True)
+    assert "continuing on the CPU" in err and "after the first chunk's D2H" in err, err
+    y = np.fromfile(fout, np.float32).view(np.complex64)
+    per = 32768 >> d
+    assert y.size == nblk * per
+    bounds = [(0, tb, 0)] + list(sched) + [(nblk, None, None)]
+    for (a, t, r), (b, _, _) in zip(bounds[:-1], bounds[1:]):
+        ref = oracle.r2iq(x[a * 65536: 4096 + b * 65536], b - a, d, t, False, r)
+        assert oracle.max_rel_err(y[a * per: b * per], ref) <= TOL, (a, b)
+
+
 def test_dropin_auto_without_gpu_uses_cpu(tmp_path, oracle):
     """SDDC_DDC_BACKEND=auto where Init finds no usable GPU (forced here with an invalid
     SDDC_DDC_DEVICE): announced on stderr, then the CPU backend produces the stream."""
