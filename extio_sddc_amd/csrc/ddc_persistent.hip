@@ -568,11 +568,25 @@ __device__ __forceinline__ float2 quarter(float2 v, int s)
     return make_float2(-v.y, v.x);
 }
 
+#ifndef SDDC_FS_USTORE
+#define SDDC_FS_USTORE 0
+#endif
 template <int QT, bool NCO, bool CS16>
 __device__ __forceinline__ void emit_frame_q(void *__restrict__ out, int fbase, int k, int t, const float2 (&u)[16],
                                              const OutArgs &oa, const NcoArgs &nco)
 {
     const __amdgpu_buffer_rsrc_t ro = buf_rsrc(static_cast<char *>(out) + (size_t)fbase * out_bytes<CS16>());
+#if SDDC_FS_USTORE
+    // all 12 stores unconditional; at k = 0 the first four go to an offset past the buffer's range
+    // (2^31 elements: discarded by the buffer unit), so the store count is the same on every path
+    const unsigned oob = k == 0 ? (CS16 ? 0x20000000u : 0x10000000u) : 0u;   // 2^31 bytes; wave-uniform
+#pragma unroll
+    for (int r = 0; r < 12; r++) {
+        float2 v = flip(quarter(u[r], QT * r), oa.lsbmask);
+        if constexpr (NCO) v = nco_mix(v, nco, fbase + t + NT * r);
+        store_iq<CS16>(v, ro, (unsigned)t, (unsigned)(NT * r) + (r < 4 ? oob : 0u), oa);
+    }
+#else
     const int r0 = k == 0 ? 4 : 0;   // wave-uniform
 #pragma unroll
     for (int r = 0; r < 12; r++) {
@@ -581,6 +595,7 @@ __device__ __forceinline__ void emit_frame_q(void *__restrict__ out, int fbase, 
         if constexpr (NCO) v = nco_mix(v, nco, fbase + t + NT * r);
         store_iq<CS16>(v, ro, (unsigned)t, (unsigned)(NT * r), oa);
     }
+#endif
 }
 
 
@@ -667,7 +682,14 @@ constexpr int kStLo = SDDC_STAMPS >= 2 ? 4 : 0;
 #ifndef SDDC_FS_BF
 #define SDDC_FS_BF 0
 #endif
-template <bool RAND, bool NCO, bool CS16>
+#ifndef SDDC_FS_DUMMY
+#define SDDC_FS_DUMMY 0
+#endif
+
+#ifndef SDDC_FS_QTT
+#define SDDC_FS_QTT 0
+#endif
+template <bool RAND, bool NCO, bool CS16, int QT = -1>
 __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
     const int *__restrict__ in32, void *__restrict__ out, int nframes,
     const float2 *__restrict__ tw_p1, const float2 *__restrict__ tw_q1,
@@ -698,14 +720,24 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
     constexpr int QLANE = 64 * SDDC_FS_QWAVE;
     const bool qw = __builtin_amdgcn_readfirstlane(tid >> 6) == SDDC_FS_QWAVE;
     FsQueue q;
-    q.init(wq, nframes, w & (FS_SHARDS - 1));   // home shard: blockIdx % 8, the XCD under round-robin placement
+#ifndef SDDC_FS_SFIRST
+#define SDDC_FS_SFIRST 0
+#endif
+    // home shard: blockIdx % 8, the XCD under round-robin placement
+    q.init(wq, nframes, w & (FS_SHARDS - 1), SDDC_FS_SFIRST ? (int)gridDim.x : 0);
+    const int f_stat = SDDC_FS_SFIRST ? fs_static_first(nframes, (int)gridDim.x, w) : -1;   // wave-uniform
+    int x[16];
+    if (f_stat >= 0) load_frame(in32, f_stat / FRAMES, f_stat - (f_stat / FRAMES) * FRAMES, x);
     if (qw) {
 #ifdef SDDC_FS_QSTATIC
         const int f_first = w < nframes ? w : -1;
 #else
-        q.take();
-        q.peek();
-        const int f_first = q.resolve();
+        int f_first = f_stat;
+        if (f_stat < 0) {
+            q.take();
+            q.peek();
+            f_first = q.resolve();
+        }
         q.take();
 #endif
         if (tid == QLANE) s_next = f_first;
@@ -728,8 +760,20 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
     __syncthreads();
     int f = s_next;
     int blk = f / FRAMES, k = f - blk * FRAMES;
-    int x[16];
-    if (f >= 0) load_frame(in32, blk, k, x);
+    if (f >= 0 && f_stat < 0) load_frame(in32, blk, k, x);
+#if SDDC_FS_DUMMY
+    // 12 stores past the output buffer's range (discarded by the buffer unit) behind the first
+    // frame's input loads: vmcnt counts loads and stores in issue order, and the waits at the
+    // frame top are computed over both ways into the loop; behind the loop's own input loads come
+    // the previous frame's 8..12 IQ stores, and without the same count here the first way forces
+    // vmcnt(0) at the top of every frame, i.e. a wait for the previous frame's stores to complete
+    {
+        const __amdgpu_buffer_rsrc_t rd = buf_rsrc(out);
+#pragma unroll
+        for (int r = 0; r < 12; r++)   // distinct offsets, or the compiler keeps only the last store
+            buf_store8(make_float2(0.f, 0.f), rd, 8u * (unsigned)tid, 0x80000000u + 8u * NT * (unsigned)r);
+    }
+#endif
     FS_STAMP_INIT();
 
     while (f >= 0) {
@@ -953,11 +997,15 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
             twiddle_g16<+1>(a, g0, cmulc(g0, rw1), cmulc(g0, rw4), rw1, rw4);   // g W^{-t}, g W^{-4t}
             dft16<+1>(a, u);
             const int fb = oblk + emit_base<HALF>(kc);
-            switch (qt) {
-            case 0: emit_frame_q<0, NCO, CS16>(out, fb, kc, t, u, oa, nco); break;
-            case 1: emit_frame_q<1, NCO, CS16>(out, fb, kc, t, u, oa, nco); break;
-            case 2: emit_frame_q<2, NCO, CS16>(out, fb, kc, t, u, oa, nco); break;
-            default: emit_frame_q<3, NCO, CS16>(out, fb, kc, t, u, oa, nco); break;
+            if constexpr (QT >= 0) {
+                emit_frame_q<QT, NCO, CS16>(out, fb, kc, t, u, oa, nco);
+            } else {
+                switch (qt) {
+                case 0: emit_frame_q<0, NCO, CS16>(out, fb, kc, t, u, oa, nco); break;
+                case 1: emit_frame_q<1, NCO, CS16>(out, fb, kc, t, u, oa, nco); break;
+                case 2: emit_frame_q<2, NCO, CS16>(out, fb, kc, t, u, oa, nco); break;
+                default: emit_frame_q<3, NCO, CS16>(out, fb, kc, t, u, oa, nco); break;
+                }
             }
         }
         FS_STAMP_FRAME_END();
@@ -1056,7 +1104,13 @@ hipError_t launch_v(const KernelTables &t, const Launch &L)
 template <bool RAND, bool NCO, bool CS16>
 hipError_t launch_fs_v(const KernelTables &t, const Launch &L, const float4 *pqf, const float2 *fsl, unsigned *wq)
 {
+#if SDDC_FS_QTT
+    const int qt = (L.tunebin >> 2) & 3;
+    auto kern = qt == 0 ? r2iq_fs_kernel<RAND, NCO, CS16, 0> : qt == 1 ? r2iq_fs_kernel<RAND, NCO, CS16, 1>
+              : qt == 2 ? r2iq_fs_kernel<RAND, NCO, CS16, 2> : r2iq_fs_kernel<RAND, NCO, CS16, 3>;
+#else
     auto kern = r2iq_fs_kernel<RAND, NCO, CS16>;
+#endif
     int occ = 0, cus = 0;
     hipError_t e = launch_geometry(t.lc, reinterpret_cast<const void *>(kern), NT, L.device, &occ, &cus);
     if (e != hipSuccess) return e;

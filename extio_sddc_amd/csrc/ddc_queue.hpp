@@ -40,19 +40,35 @@ __device__ __forceinline__ int fs_shard_lo(int nframes, int s) { return (nframes
 // return right there, a device-scope round trip (~1200 cycles of the queue wave per frame at
 // inverse pass 0, profiles/r03/stamps/stamps_q8.txt).
 constexpr unsigned FS_OOB = 0x80000000u;   // a buffer offset past the queue slot's range
+// The first frame of every workgroup can also be static: the first pre_s = min(size, workgroups
+// homed there) frames of shard s go to its home workgroups in blockIdx order (frame lo_s + blockIdx
+// / 8), and the shard's tickets count from there.  The first frame's input then loads at once,
+// with no device-scope atomic round trip in front of it (grid = 0: every frame from the queue).
+__device__ __forceinline__ int fs_shard_pre(int nframes, int grid, int s)
+{
+    const int cnt = fs_shard_lo(nframes, s + 1) - fs_shard_lo(nframes, s);
+    const int nwg = (grid - s + FS_SHARDS - 1) / FS_SHARDS;
+    return cnt < nwg ? cnt : nwg;
+}
+__device__ __forceinline__ int fs_static_first(int nframes, int grid, int w)
+{
+    const int s = w & (FS_SHARDS - 1), j = w / FS_SHARDS;
+    return j < fs_shard_pre(nframes, grid, s) ? fs_shard_lo(nframes, s) + j : -1;
+}
 struct FsQueue {
     __amdgpu_buffer_rsrc_t rq;   // the queue slot as a buffer (kFsQueueWords words)
-    int nframes, sh0;
+    int nframes, sh0, grid;
     int shn;        // shard of the pending ticket (8: every shard dry)
     int lo, cnt;    // first frame and size of that shard (cnt = 0 once every shard is dry)
     int tk;         // lane 0: the pending ticket
     int pv;         // its value, read by peek()
 
-    __device__ __forceinline__ void init(unsigned *wq, int nframes_, int home)
+    __device__ __forceinline__ void init(unsigned *wq, int nframes_, int home, int grid_ = 0)
     {
         rq = __builtin_amdgcn_make_buffer_rsrc(wq, (short)0, 4 * kFsQueueWords, 0x00020000);
         nframes = nframes_;
         sh0 = home;
+        grid = grid_;
         set_shard(0);
     }
     __device__ __forceinline__ void set_shard(int sh)
@@ -61,6 +77,11 @@ struct FsQueue {
         const int s = (sh0 + sh) & (FS_SHARDS - 1);
         lo = fs_shard_lo(nframes, s);
         cnt = sh < FS_SHARDS ? fs_shard_lo(nframes, s + 1) - lo : 0;
+        if (grid) {   // the static first frames
+            const int pre = fs_shard_pre(nframes, grid, s);
+            lo += pre;
+            cnt -= pre;
+        }
     }
     // takes a ticket of the current shard (lane 0; no wait).  Called by the whole wave; the
     // offset is recomputed here (a few scalar instructions and one select) rather than kept in
