@@ -100,37 +100,8 @@ __device__ __forceinline__ void table_twiddle(float2 *a, const float2 *tbl, int 
     }
 }
 
-// the 15 pass-1 table twiddles of lane x15, read before the pass's data (one memory clobber after
-// them), so that all of them are in flight at once
-__device__ __forceinline__ void tw_first(float2 (&tw)[15], const float2 *twl, int x15)
-{
-#pragma unroll
-    for (int r = 1; r < 16; r++) tw[r - 1] = twl[(r - 1) * 16 + x15];
-    asm volatile("" ::: "memory");
-}
-// Pins the values of DFT-4 group g (r = g + 4 j) and their twiddles: an empty volatile asm that
-// reads and rewrites them.  Volatile asms keep their program order, so pins placed after the last
-// read of a pass hold every product behind the issue of all the pass's reads: one LDS round trip
-// per pass instead of the compiler's read / lgkmcnt(0) / product chain.
-__device__ __forceinline__ void pin_group(float2 (&a)[16], float2 (&tw)[15], int g)
-{
-    if (g == 0) {
-        asm volatile("" : "+v"(a[0].x), "+v"(a[0].y), "+v"(a[4].x), "+v"(a[4].y), "+v"(a[8].x), "+v"(a[8].y),
-                     "+v"(a[12].x), "+v"(a[12].y), "+v"(tw[3].x), "+v"(tw[3].y), "+v"(tw[7].x), "+v"(tw[7].y),
-                     "+v"(tw[11].x), "+v"(tw[11].y));
-    } else {
-        asm volatile("" : "+v"(a[g].x), "+v"(a[g].y), "+v"(a[g + 4].x), "+v"(a[g + 4].y), "+v"(a[g + 8].x),
-                     "+v"(a[g + 8].y), "+v"(a[g + 12].x), "+v"(a[g + 12].y), "+v"(tw[g - 1].x), "+v"(tw[g - 1].y),
-                     "+v"(tw[g + 3].x), "+v"(tw[g + 3].y), "+v"(tw[g + 7].x), "+v"(tw[g + 7].y),
-                     "+v"(tw[g + 11].x), "+v"(tw[g + 11].y));
-    }
-}
-
-#ifndef SDDC_P_TWF
-#define SDDC_P_TWF 0
-#endif
 template <int D, bool RAND, bool NCO, bool CS16>
-__global__ __launch_bounds__(NT, (D <= 1 || ((SDDC_P_TWF >> D) & 1)) ? 4 : 2) void r2iq_persistent_kernel(
+__global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
     const int *__restrict__ in32, void *__restrict__ out, int nframes,
     const float2 *__restrict__ tw_p1, const float2 *__restrict__ tw_q1,
     const float2 *__restrict__ rec_f, const float2 *__restrict__ rec_i, const float2 *__restrict__ tw4096,
@@ -147,7 +118,6 @@ __global__ __launch_bounds__(NT, (D <= 1 || ((SDDC_P_TWF >> D) & 1)) ? 4 : 2) vo
     // (profiles/r02/ab/prune_d3_6.txt, prune_d2.txt).
     constexpr bool PRUNE = N <= 1024;
     constexpr bool TW_EARLY = D <= 1;   // (held to 128 VGPRs by the launch bounds)
-    constexpr bool P_TWF = (SDDC_P_TWF >> D) & 1;
     // st_row stores: the forward pass-0 rows at d >= 1 only (at d = 0 1.2-1.7 % slower), the
     // other rows at every d (inverse pass-0 rows at d = 0: +0.9-1.3 % on one box, xst_d0_parts.txt,
     // neutral on another, xst_inv0_confirm.txt; bit-identical, 15 VALU fewer)
@@ -301,22 +271,9 @@ __global__ __launch_bounds__(NT, (D <= 1 || ((SDDC_P_TWF >> D) & 1)) ? 4 : 2) vo
         // ---- forward pass 1 (R16, NS16): table twiddles W_256^{(t%16) r} ----
         {
             float2 a[16];
-            if constexpr (P_TWF) {
-                float2 tw[15];
-                tw_first(tw, twl, x15);
 #pragma unroll
-                for (int g = 0; g < 4; g++)
-#pragma unroll
-                    for (int j = 0; j < 4; j++) XRD(a[g + 4 * j], w0[sT + NT * (g + 4 * j)]);
-#pragma unroll
-                for (int g = 0; g < 4; g++) pin_group(a, tw, g);
-#pragma unroll
-                for (int r = 1; r < 16; r++) a[r] = TW<-1>(a[r], tw[r - 1]);
-            } else {
-#pragma unroll
-                for (int r = 0; r < 16; r++) XRD(a[r], w0[sT + NT * r]);
-                table_twiddle<-1, TW_EARLY>(a, twl, 16, x15);
-            }
+            for (int r = 0; r < 16; r++) XRD(a[r], w0[sT + NT * r]);
+            table_twiddle<-1, TW_EARLY>(a, twl, 16, x15);
             dft16<-1>(a, v);
         }
         __syncthreads();
@@ -568,25 +525,11 @@ __device__ __forceinline__ float2 quarter(float2 v, int s)
     return make_float2(-v.y, v.x);
 }
 
-#ifndef SDDC_FS_USTORE
-#define SDDC_FS_USTORE 0
-#endif
 template <int QT, bool NCO, bool CS16>
 __device__ __forceinline__ void emit_frame_q(void *__restrict__ out, int fbase, int k, int t, const float2 (&u)[16],
                                              const OutArgs &oa, const NcoArgs &nco)
 {
     const __amdgpu_buffer_rsrc_t ro = buf_rsrc(static_cast<char *>(out) + (size_t)fbase * out_bytes<CS16>());
-#if SDDC_FS_USTORE
-    // all 12 stores unconditional; at k = 0 the first four go to an offset past the buffer's range
-    // (2^31 elements: discarded by the buffer unit), so the store count is the same on every path
-    const unsigned oob = k == 0 ? (CS16 ? 0x20000000u : 0x10000000u) : 0u;   // 2^31 bytes; wave-uniform
-#pragma unroll
-    for (int r = 0; r < 12; r++) {
-        float2 v = flip(quarter(u[r], QT * r), oa.lsbmask);
-        if constexpr (NCO) v = nco_mix(v, nco, fbase + t + NT * r);
-        store_iq<CS16>(v, ro, (unsigned)t, (unsigned)(NT * r) + (r < 4 ? oob : 0u), oa);
-    }
-#else
     const int r0 = k == 0 ? 4 : 0;   // wave-uniform
 #pragma unroll
     for (int r = 0; r < 12; r++) {
@@ -595,7 +538,6 @@ __device__ __forceinline__ void emit_frame_q(void *__restrict__ out, int fbase, 
         if constexpr (NCO) v = nco_mix(v, nco, fbase + t + NT * r);
         store_iq<CS16>(v, ro, (unsigned)t, (unsigned)(NT * r), oa);
     }
-#endif
 }
 
 
@@ -676,20 +618,7 @@ constexpr int kStLo = SDDC_STAMPS >= 2 ? 4 : 0;
 #define FS_STAMP_WRITE(wg, tid, nfr) (void)0
 #endif
 
-#ifndef SDDC_FS_TWF
-#define SDDC_FS_TWF 0
-#endif
-#ifndef SDDC_FS_BF
-#define SDDC_FS_BF 0
-#endif
-#ifndef SDDC_FS_DUMMY
-#define SDDC_FS_DUMMY 0
-#endif
-
-#ifndef SDDC_FS_QTT
-#define SDDC_FS_QTT 0
-#endif
-template <bool RAND, bool NCO, bool CS16, int QT = -1>
+template <bool RAND, bool NCO, bool CS16>
 __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
     const int *__restrict__ in32, void *__restrict__ out, int nframes,
     const float2 *__restrict__ tw_p1, const float2 *__restrict__ tw_q1,
@@ -720,20 +649,23 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
     constexpr int QLANE = 64 * SDDC_FS_QWAVE;
     const bool qw = __builtin_amdgcn_readfirstlane(tid >> 6) == SDDC_FS_QWAVE;
     FsQueue q;
-#ifndef SDDC_FS_SFIRST
-#define SDDC_FS_SFIRST 0
+    // home shard: blockIdx % 8, the XCD under round-robin placement.  The first frame is static
+    // (fs_static_first): its input loads go out at once, ahead of the table copies, with no device-
+    // scope atomic round trip in front of them (+0.4-1.7 %, profiles/r03/ab/fs_static_first*.txt)
+    q.init(wq, nframes, w & (FS_SHARDS - 1), (int)gridDim.x);
+#ifdef SDDC_FS_QSTATIC
+    const int f_stat = -1;
+#else
+    const int f_stat = fs_static_first(nframes, (int)gridDim.x, w);   // wave-uniform; -1: none
 #endif
-    // home shard: blockIdx % 8, the XCD under round-robin placement
-    q.init(wq, nframes, w & (FS_SHARDS - 1), SDDC_FS_SFIRST ? (int)gridDim.x : 0);
-    const int f_stat = SDDC_FS_SFIRST ? fs_static_first(nframes, (int)gridDim.x, w) : -1;   // wave-uniform
     int x[16];
-    if (f_stat >= 0) load_frame(in32, f_stat / FRAMES, f_stat - (f_stat / FRAMES) * FRAMES, x);
+    if (f_stat >= 0) load_frame(in32, f_stat / FRAMES, f_stat % FRAMES, x);
     if (qw) {
 #ifdef SDDC_FS_QSTATIC
         const int f_first = w < nframes ? w : -1;
 #else
         int f_first = f_stat;
-        if (f_stat < 0) {
+        if (f_stat < 0) {   // only when a shard has fewer frames than workgroups (small batches)
             q.take();
             q.peek();
             f_first = q.resolve();
@@ -761,19 +693,6 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
     int f = s_next;
     int blk = f / FRAMES, k = f - blk * FRAMES;
     if (f >= 0 && f_stat < 0) load_frame(in32, blk, k, x);
-#if SDDC_FS_DUMMY
-    // 12 stores past the output buffer's range (discarded by the buffer unit) behind the first
-    // frame's input loads: vmcnt counts loads and stores in issue order, and the waits at the
-    // frame top are computed over both ways into the loop; behind the loop's own input loads come
-    // the previous frame's 8..12 IQ stores, and without the same count here the first way forces
-    // vmcnt(0) at the top of every frame, i.e. a wait for the previous frame's stores to complete
-    {
-        const __amdgpu_buffer_rsrc_t rd = buf_rsrc(out);
-#pragma unroll
-        for (int r = 0; r < 12; r++)   // distinct offsets, or the compiler keeps only the last store
-            buf_store8(make_float2(0.f, 0.f), rd, 8u * (unsigned)tid, 0x80000000u + 8u * NT * (unsigned)r);
-    }
-#endif
     FS_STAMP_INIT();
 
     while (f >= 0) {
@@ -803,32 +722,13 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
         FS_SYNC(0);   // the previous frame's last LDS reads are done
 #pragma unroll
         for (int r = 0; r < 16; r++) lds[16 * t + (r ^ x15)] = v[r];
-#if SDDC_FS_TWF >= 2
-        float2 tw1[15];
-        tw_first(tw1, twl, x15);
-#endif
         FS_SYNC(1);
         // ---- forward pass 1 (R16, NS16): table twiddles W_256^{(t%16) r} ----
         {
             float2 a[16];
-#if SDDC_FS_TWF == 1
-            float2 tw1[15];
-            tw_first(tw1, twl, x15);
-#endif
-#if SDDC_FS_TWF
-#pragma unroll
-            for (int g = 0; g < 4; g++)
-#pragma unroll
-                for (int j = 0; j < 4; j++) XRD(a[g + 4 * j], lds[sT + NT * (g + 4 * j)]);
-#pragma unroll
-            for (int g = 0; g < 4; g++) pin_group(a, tw1, g);
-#pragma unroll
-            for (int r = 1; r < 16; r++) a[r] = TW<-1>(a[r], tw1[r - 1]);
-#else
 #pragma unroll
             for (int r = 0; r < 16; r++) XRD(a[r], lds[sT + NT * r]);
             table_twiddle<-1, true>(a, twl, 16, x15);
-#endif
             dft16<-1>(a, v);
         }
         FS_SYNC(2);
@@ -855,15 +755,9 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
         {
             float2 a[16];
             const int sC = swz(c);
-#if SDDC_FS_BF   // the twiddle bases first: their powers are formed while the data reads are in flight
-            const float2 fw1 = wtab[c], fw4 = wtab[NT + c];   // W^c, W^{4c}
-            asm volatile("" ::: "memory");
-#endif
 #pragma unroll
             for (int r = 0; r < 16; r++) XRD(a[r], lds[sC + NT * r]);
-#if !SDDC_FS_BF
             const float2 fw1 = wtab[c], fw4 = wtab[NT + c];   // W^c, W^{4c}
-#endif
             twiddle_rec16<-1>(a, fw1, fw4);
             dft16<-1>(a, v);
         }
@@ -947,28 +841,10 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
             // element j + 256 r was stored by inverse pass-0 column (j >> 4) + 16 r under the key
             // swz(column) & 15 = (j >> 4) ^ r: byte (8 sT ^ 8 r) + 2048 r, one v_xor per read
             const unsigned sT8 = 8u * (unsigned)sT;
-#if SDDC_FS_TWF
-            float2 tw2[15];
-            tw_first(tw2, twl, x15);
-#endif
-#if SDDC_FS_TWF
-#pragma unroll
-            for (int g = 0; g < 4; g++)
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    const unsigned r = (unsigned)(g + 4 * j);
-                    XRD(a[r], *reinterpret_cast<const float2 *>(reinterpret_cast<const char *>(lds) + ((sT8 ^ (8u * r)) + 2048u * r)));
-                }
-#pragma unroll
-            for (int g = 0; g < 4; g++) pin_group(a, tw2, g);
-#pragma unroll
-            for (int r = 1; r < 16; r++) a[r] = TW<+1>(a[r], tw2[r - 1]);
-#else
 #pragma unroll
             for (int r = 0; r < 16; r++)
                 XRD(a[r], *reinterpret_cast<const float2 *>(reinterpret_cast<const char *>(lds) + ((sT8 ^ (8u * r)) + 2048u * r)));
             table_twiddle<+1, true>(a, twl, 16, x15);
-#endif
             dft16<+1>(a, u);
         }
         FS_SYNC(6);
@@ -985,27 +861,17 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
         // ---- inverse pass 2 (R16, NS256): twiddles g_t W^{-t r}, quarter turns, overlap-discard ----
         {
             float2 a[16];
-#if SDDC_FS_BF
-            const float2 rw1 = wtab[t], rw4 = wtab[NT + t], g0 = gtab[t];   // W^t, W^{4t}, g_t
-            asm volatile("" ::: "memory");
-#endif
 #pragma unroll
             for (int r = 0; r < 16; r++) XRD(a[r], lds[sT + NT * r]);
-#if !SDDC_FS_BF
             const float2 rw1 = wtab[t], rw4 = wtab[NT + t], g0 = gtab[t];   // W^t, W^{4t}, g_t
-#endif
             twiddle_g16<+1>(a, g0, cmulc(g0, rw1), cmulc(g0, rw4), rw1, rw4);   // g W^{-t}, g W^{-4t}
             dft16<+1>(a, u);
             const int fb = oblk + emit_base<HALF>(kc);
-            if constexpr (QT >= 0) {
-                emit_frame_q<QT, NCO, CS16>(out, fb, kc, t, u, oa, nco);
-            } else {
-                switch (qt) {
-                case 0: emit_frame_q<0, NCO, CS16>(out, fb, kc, t, u, oa, nco); break;
-                case 1: emit_frame_q<1, NCO, CS16>(out, fb, kc, t, u, oa, nco); break;
-                case 2: emit_frame_q<2, NCO, CS16>(out, fb, kc, t, u, oa, nco); break;
-                default: emit_frame_q<3, NCO, CS16>(out, fb, kc, t, u, oa, nco); break;
-                }
+            switch (qt) {
+            case 0: emit_frame_q<0, NCO, CS16>(out, fb, kc, t, u, oa, nco); break;
+            case 1: emit_frame_q<1, NCO, CS16>(out, fb, kc, t, u, oa, nco); break;
+            case 2: emit_frame_q<2, NCO, CS16>(out, fb, kc, t, u, oa, nco); break;
+            default: emit_frame_q<3, NCO, CS16>(out, fb, kc, t, u, oa, nco); break;
             }
         }
         FS_STAMP_FRAME_END();
@@ -1104,13 +970,7 @@ hipError_t launch_v(const KernelTables &t, const Launch &L)
 template <bool RAND, bool NCO, bool CS16>
 hipError_t launch_fs_v(const KernelTables &t, const Launch &L, const float4 *pqf, const float2 *fsl, unsigned *wq)
 {
-#if SDDC_FS_QTT
-    const int qt = (L.tunebin >> 2) & 3;
-    auto kern = qt == 0 ? r2iq_fs_kernel<RAND, NCO, CS16, 0> : qt == 1 ? r2iq_fs_kernel<RAND, NCO, CS16, 1>
-              : qt == 2 ? r2iq_fs_kernel<RAND, NCO, CS16, 2> : r2iq_fs_kernel<RAND, NCO, CS16, 3>;
-#else
     auto kern = r2iq_fs_kernel<RAND, NCO, CS16>;
-#endif
     int occ = 0, cus = 0;
     hipError_t e = launch_geometry(t.lc, reinterpret_cast<const void *>(kern), NT, L.device, &occ, &cus);
     if (e != hipSuccess) return e;
