@@ -101,6 +101,20 @@ def main():
             if m.any():
                 print(f"    CU slot (HW_ID tg_id) {s_}: {m.sum():4d} workgroups, end p50 {np.median(re_us[m]):.1f} us, "
                       f"min {re_us[m].min():.1f} max {re_us[m].max():.1f}")
+        # which SIMD each wave index of a workgroup runs on (HW_ID SIMD_ID, bits 5:4), and, over the
+        # workgroups sharing a CU (SE, SH, CU ids), whether wave 0 of every workgroup lands on one SIMD
+        hwa = st[:, :, 2 * SEGS + 6].astype(np.int64)
+        simd = (hwa >> 4) & 3
+        for wv in range(4):
+            cnt = np.bincount(simd[:, wv], minlength=4)
+            print(f"    wave {wv}: SIMD histogram {cnt.tolist()}")
+        cu = (hwa[:, 0] >> 8) & 0x7F   # CU_ID, SH_ID, SE_ID
+        same = []
+        for c in np.unique(cu):
+            m = cu == c
+            same.append(len(np.unique(simd[m, 0])))
+        print(f"    distinct SIMDs holding wave 0 among the workgroups of one CU id: "
+              f"{np.bincount(np.array(same), minlength=5)[1:].tolist()} (count of CU ids with 1, 2, 3, 4)")
         lo = 4 if which >= 2 else 0
         if which == 3:
             for i, what in enumerate(("resolve", "s_next write", "next ticket", "ticket read (frame top)")):
