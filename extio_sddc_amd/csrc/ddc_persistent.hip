@@ -148,7 +148,14 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
     __shared__ __attribute__((aligned(16))) float2 lds[HALF];
     // pass-1 twiddle tables, copied once per workgroup: [15][16] forward, [15][S] inverse
     constexpr int SQ = N >= 512 ? N / 256 : N / 16;
-    __shared__ __attribute__((aligned(16))) float2 twl[15 * 16 + 15 * SQ];
+    // d = 4 (N = 256): the inverse runs as four radix-4 passes on the 64 lanes of wave 0 (below);
+    // their twiddles W_{4 Ns}^{k r} (Ns = 4, 16, 64; k < Ns; r = 1..3) take the inverse table's place
+#ifndef SDDC_P_R4TAIL
+#define SDDC_P_R4TAIL 1
+#endif
+    constexpr bool R4T = SDDC_P_R4TAIL && N == 256;
+    constexpr int TWQ = R4T ? 3 * (4 + 16 + 64) : 15 * SQ;
+    __shared__ __attribute__((aligned(16))) float2 twl[15 * 16 + TWQ];
     float2 *const w0 = lds, *const w1 = lds;   // the pass buffers (one 32 KB frame buffer)
     // d >= 2: the inverse's last passes run on one wave (N/16 <= 64 butterflies), so they are
     // ordered within that wave (wave_lds_sync) and the other waves go on to the next frame's
@@ -210,8 +217,18 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
             iw4_ = rec_i[NT + tid];
         }
     }
-    for (int i = tid; i < 15 * 16 + 15 * SQ; i += NT)
-        twl[i] = i < 15 * 16 ? tw_p1[i] : tw_q1[i - 15 * 16];   // visible after the first frame's pass-0 barrier
+    for (int i = tid; i < 15 * 16 + TWQ; i += NT) {
+        if (!R4T || i < 15 * 16) {
+            twl[i] = i < 15 * 16 ? tw_p1[i] : tw_q1[i - 15 * 16];   // visible after the first frame's pass-0 barrier
+        } else {
+            // segment of pass p (Ns = 4^p) at 12 (Ns - 1) / 3... : Ns = 4: [0, 12), 16: [12, 60), 64: [60, 252)
+            const int e = i - 15 * 16;
+            const int ns = e < 12 ? 4 : e < 60 ? 16 : 64;
+            const int o = e - (ns == 4 ? 0 : ns == 16 ? 12 : 60);
+            const int r = o / ns + 1, kk = o % ns;
+            twl[i] = tw4096[(kk * r * (1024 / ns)) & (HALF - 1)];   // forward W_{4 Ns}^{k r}
+        }
+    }
 
     __syncthreads();   // s_first, s_next
     int f = s_first;
@@ -412,6 +429,55 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
                 const int bin = tunebin + m - (m >= N / 2 ? N : 0);
                 tv = split_pq(w0[bin & (HALF - 1)], w0[(HALF - bin) & (HALF - 1)], pqz[m]);
             }
+            if constexpr (R4T) {
+                // d = 4: the 256-point inverse as four radix-4 Stockham passes on the 64 lanes of
+                // wave 0 (the [16, 16] form below keeps 16 lanes busy: its two DFT-16 passes cost
+                // d = 4 11 % of the launch, a timing-only build without them measured).  LDS
+                // element e at e ^ ((e >> 2) & 31): conflict-free for every read and write pattern
+                // of the four passes (model: tools/r4_tail_model.py).
+                if (t < N) sb[t ^ ((t >> 2) & 31)] = tv;
+                __syncthreads();
+                if (t < 64) {
+                    float2 a[4], u[4];
+#pragma unroll
+                    for (int p = 0; p < 4; p++) {
+                        const int ns = 1 << (2 * p);
+                        const int kk = t & (ns - 1);
+#pragma unroll
+                        for (int r = 0; r < 4; r++) {
+                            const int e = t + 64 * r;
+                            a[r] = sb[e ^ ((e >> 2) & 31)];
+                        }
+                        if (p > 0) {
+                            const int seg = 15 * 16 + (ns == 4 ? 0 : ns == 16 ? 12 : 60);
+#pragma unroll
+                            for (int r = 1; r < 4; r++) a[r] = TW<+1>(a[r], twl[seg + (r - 1) * ns + kk]);
+                        }
+                        dft4<+1>(a, u);
+                        if (p < 3) {
+                            wave_lds_sync();   // this wave's reads of the pass are done
+#pragma unroll
+                            for (int r = 0; r < 4; r++) {
+                                const int e = (t >> (2 * p)) * 4 * ns + kk + ns * r;
+                                sb[e ^ ((e >> 2) & 31)] = u[r];
+                            }
+                            wave_lds_sync();
+                        }
+                    }
+                    // u[r] = y[t + 64 r]; kept: y[0, 192) (k >= 1), y[64, 192) (k = 0)
+                    const int fbase = oblk + emit_base<N>(kc);
+                    const __amdgpu_buffer_rsrc_t ro = buf_rsrc(static_cast<char *>(out) + (size_t)fbase * out_bytes<CS16>());
+#pragma unroll
+                    for (int r = 0; r < 3; r++) {
+                        if (r == 0 && kc == 0) continue;
+                        float2 vv = flip(u[r], oa.lsbmask);
+                        if constexpr (NCO) vv = nco_mix(vv, nco, fbase + t + 64 * r);
+                        store_iq<CS16>(vv, ro, (unsigned)t, (unsigned)(64 * r), oa);
+                    }
+                }
+                f = fn;
+                continue;
+            }
             // SEPB: the bins go to sb, and wave 0 alone runs the two passes below on sb
             float2 *const v0 = SEPB ? sb : w1, *const v1 = SEPB ? sb : w0;
             if constexpr (!SEPB) __syncthreads();
@@ -422,7 +488,12 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
                 float2 a[R0];
 #pragma unroll
                 for (int r = 0; r < R0; r++) a[r] = LX(v0, t, 16 * r);
+#ifdef SDDC_FAKE_TAIL   // timing only: no inverse arithmetic at N <= 256 (wrong results)
+#pragma unroll
+                for (int r = 0; r < R0; r++) u[r] = a[r];
+#else
                 dft<R0, +1>(a, u);
+#endif
             }
             if constexpr (SEPB) wave_lds_sync();
             else __syncthreads();
@@ -437,9 +508,14 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
                 float2 a[16];
 #pragma unroll
                 for (int r = 0; r < 16; r++) a[r] = LX(v1, t, NB * r);
+#ifdef SDDC_FAKE_TAIL
+#pragma unroll
+                for (int r = 0; r < 16; r++) u[r] = a[r];
+#else
 #pragma unroll
                 for (int r = 1; r < 16; r++) a[r] = TW<+1>(a[r], twl[15 * 16 + (r - 1) * NB + t]);
                 dft16<+1>(a, u);
+#endif
                 emit_frame<NB, NCO, CS16>(out, oblk + emit_base<N>(kc), kc, t, u, oa, nco);
             }
         }
