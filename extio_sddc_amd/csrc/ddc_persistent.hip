@@ -100,6 +100,67 @@ __device__ __forceinline__ void table_twiddle(float2 *a, const float2 *tbl, int 
     }
 }
 
+// d >= 4 (N = 256, 128, 64): the N-point inverse as mixed-radix Stockham passes on the lanes of
+// wave 0, radix schedule 4-4-4-4, 8-4-4, 4-4-4.  The pass of radix R after a span Ns runs on
+// threads j < N / R: reads elements j + (N / R) r, twiddles W_{R Ns}^{-k r} (k = j mod Ns),
+// inverse DFT-R, writes (j / Ns) R Ns + k + Ns r; the last pass leaves y[j + (N / 4) r] in
+// registers.  LDS element e sits at e ^ ((e >> s) & 31) (s = 1 at N = 64, else 2): conflict-
+// free for every read and write pattern (tools/r4_tail_model.py, which also checks the passes
+// against numpy).  The [N/16, 16] form it replaces kept 16 lanes busy (d = 4) or fewer; its two
+// passes cost 8-11 % of the launch at d = 4..6 (timing-only build, profiles/r03/ab).
+template <int N> constexpr int tail_radix(int p) { return (N == 128 && p == 0) ? 8 : 4; }
+template <int N> constexpr int tail_passes() { return N == 256 ? 4 : 3; }
+template <int N> constexpr int tail_ns(int p)
+{
+    int ns = 1;
+    for (int q = 0; q < p; q++) ns *= tail_radix<N>(q);
+    return ns;
+}
+template <int N> constexpr int tail_twoff(int p)   // first twiddle of pass p in the tail's table
+{
+    int o = 0;
+    for (int q = 1; q < p; q++) o += (tail_radix<N>(q) - 1) * tail_ns<N>(q);
+    return o;
+}
+template <int N> constexpr int tail_twn() { return tail_twoff<N>(tail_passes<N>()); }
+template <int N> __device__ __forceinline__ int tail_swz(int e) { return e ^ ((e >> (N == 64 ? 1 : 2)) & 31); }
+
+// the forward twiddle W_{R Ns}^{k r} of entry e of the tail's table
+template <int N> __device__ __forceinline__ float2 tail_twiddle(const float2 *__restrict__ tw4096, int e)
+{
+    int p = 1;
+    while (p + 1 < tail_passes<N>() && e >= tail_twoff<N>(p + 1)) p++;
+    const int ns = tail_ns<N>(p), R = tail_radix<N>(p);
+    const int o = e - tail_twoff<N>(p), r = o / ns + 1, kk = o % ns;
+    return tw4096[(kk * r * (HALF / (R * ns))) & (HALF - 1)];
+}
+
+template <int N, int P>
+__device__ __forceinline__ void tail_pass(float2 *sb, const float2 *twq, int t, float2 (&u)[8])
+{
+    constexpr int R = tail_radix<N>(P), NS = tail_ns<N>(P), T = N / R;
+    const int kk = t & (NS - 1);
+    if (t < T) {
+        float2 a[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) a[r] = sb[tail_swz<N>(t + T * r)];
+        if constexpr (P > 0) {
+#pragma unroll
+            for (int r = 1; r < R; r++) a[r] = TW<+1>(a[r], twq[tail_twoff<N>(P) + (r - 1) * NS + kk]);
+        }
+        if constexpr (R == 8) dft8<+1>(a, u);
+        else dft4<+1>(a, u);
+    }
+    if constexpr (P + 1 < tail_passes<N>()) {
+        wave_lds_sync();   // this wave's reads of the pass are done
+        if (t < T) {
+#pragma unroll
+            for (int r = 0; r < R; r++) sb[tail_swz<N>((t / NS) * R * NS + kk + NS * r)] = u[r];
+        }
+        wave_lds_sync();
+    }
+}
+
 template <int D, bool RAND, bool NCO, bool CS16>
 __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
     const int *__restrict__ in32, void *__restrict__ out, int nframes,
@@ -148,13 +209,13 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
     __shared__ __attribute__((aligned(16))) float2 lds[HALF];
     // pass-1 twiddle tables, copied once per workgroup: [15][16] forward, [15][S] inverse
     constexpr int SQ = N >= 512 ? N / 256 : N / 16;
-    // d = 4 (N = 256): the inverse runs as four radix-4 passes on the 64 lanes of wave 0 (below);
-    // their twiddles W_{4 Ns}^{k r} (Ns = 4, 16, 64; k < Ns; r = 1..3) take the inverse table's place
+    // d >= 4: the inverse runs as Stockham passes on wave 0 (tail_pass); their twiddles take the
+    // inverse table's place
 #ifndef SDDC_P_R4TAIL
 #define SDDC_P_R4TAIL 1
 #endif
-    constexpr bool R4T = SDDC_P_R4TAIL && N == 256;
-    constexpr int TWQ = R4T ? 3 * (4 + 16 + 64) : 15 * SQ;
+    constexpr bool R4T = SDDC_P_R4TAIL && N <= 256;
+    constexpr int TWQ = R4T ? tail_twn<N>() : 15 * SQ;
     __shared__ __attribute__((aligned(16))) float2 twl[15 * 16 + TWQ];
     float2 *const w0 = lds, *const w1 = lds;   // the pass buffers (one 32 KB frame buffer)
     // d >= 2: the inverse's last passes run on one wave (N/16 <= 64 butterflies), so they are
@@ -221,12 +282,7 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
         if (!R4T || i < 15 * 16) {
             twl[i] = i < 15 * 16 ? tw_p1[i] : tw_q1[i - 15 * 16];   // visible after the first frame's pass-0 barrier
         } else {
-            // segment of pass p (Ns = 4^p) at 12 (Ns - 1) / 3... : Ns = 4: [0, 12), 16: [12, 60), 64: [60, 252)
-            const int e = i - 15 * 16;
-            const int ns = e < 12 ? 4 : e < 60 ? 16 : 64;
-            const int o = e - (ns == 4 ? 0 : ns == 16 ? 12 : 60);
-            const int r = o / ns + 1, kk = o % ns;
-            twl[i] = tw4096[(kk * r * (1024 / ns)) & (HALF - 1)];   // forward W_{4 Ns}^{k r}
+            if constexpr (R4T) twl[i] = tail_twiddle<N>(tw4096, i - 15 * 16);
         }
     }
 
@@ -430,49 +486,27 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
                 tv = split_pq(w0[bin & (HALF - 1)], w0[(HALF - bin) & (HALF - 1)], pqz[m]);
             }
             if constexpr (R4T) {
-                // d = 4: the 256-point inverse as four radix-4 Stockham passes on the 64 lanes of
-                // wave 0 (the [16, 16] form below keeps 16 lanes busy: its two DFT-16 passes cost
-                // d = 4 11 % of the launch, a timing-only build without them measured).  LDS
-                // element e at e ^ ((e >> 2) & 31): conflict-free for every read and write pattern
-                // of the four passes (model: tools/r4_tail_model.py).
-                if (t < N) sb[t ^ ((t >> 2) & 31)] = tv;
+                if (t < N) sb[tail_swz<N>(t)] = tv;
                 __syncthreads();
                 if (t < 64) {
-                    float2 a[4], u[4];
+                    float2 u[8];
+                    const float2 *twq = twl + 15 * 16;
+                    tail_pass<N, 0>(sb, twq, t, u);
+                    tail_pass<N, 1>(sb, twq, t, u);
+                    tail_pass<N, 2>(sb, twq, t, u);
+                    if constexpr (tail_passes<N>() == 4) tail_pass<N, 3>(sb, twq, t, u);
+                    // u[r] = y[t + (N / 4) r]; kept: y[0, 3N/4) (k >= 1), y[N/4, 3N/4) (k = 0)
+                    constexpr int TL = N / 4;
+                    if (t < TL) {
+                        const int fbase = oblk + emit_base<N>(kc);
+                        const __amdgpu_buffer_rsrc_t ro = buf_rsrc(static_cast<char *>(out) + (size_t)fbase * out_bytes<CS16>());
 #pragma unroll
-                    for (int p = 0; p < 4; p++) {
-                        const int ns = 1 << (2 * p);
-                        const int kk = t & (ns - 1);
-#pragma unroll
-                        for (int r = 0; r < 4; r++) {
-                            const int e = t + 64 * r;
-                            a[r] = sb[e ^ ((e >> 2) & 31)];
+                        for (int r = 0; r < 3; r++) {
+                            if (r == 0 && kc == 0) continue;
+                            float2 vv = flip(u[r], oa.lsbmask);
+                            if constexpr (NCO) vv = nco_mix(vv, nco, fbase + t + TL * r);
+                            store_iq<CS16>(vv, ro, (unsigned)t, (unsigned)(TL * r), oa);
                         }
-                        if (p > 0) {
-                            const int seg = 15 * 16 + (ns == 4 ? 0 : ns == 16 ? 12 : 60);
-#pragma unroll
-                            for (int r = 1; r < 4; r++) a[r] = TW<+1>(a[r], twl[seg + (r - 1) * ns + kk]);
-                        }
-                        dft4<+1>(a, u);
-                        if (p < 3) {
-                            wave_lds_sync();   // this wave's reads of the pass are done
-#pragma unroll
-                            for (int r = 0; r < 4; r++) {
-                                const int e = (t >> (2 * p)) * 4 * ns + kk + ns * r;
-                                sb[e ^ ((e >> 2) & 31)] = u[r];
-                            }
-                            wave_lds_sync();
-                        }
-                    }
-                    // u[r] = y[t + 64 r]; kept: y[0, 192) (k >= 1), y[64, 192) (k = 0)
-                    const int fbase = oblk + emit_base<N>(kc);
-                    const __amdgpu_buffer_rsrc_t ro = buf_rsrc(static_cast<char *>(out) + (size_t)fbase * out_bytes<CS16>());
-#pragma unroll
-                    for (int r = 0; r < 3; r++) {
-                        if (r == 0 && kc == 0) continue;
-                        float2 vv = flip(u[r], oa.lsbmask);
-                        if constexpr (NCO) vv = nco_mix(vv, nco, fbase + t + 64 * r);
-                        store_iq<CS16>(vv, ro, (unsigned)t, (unsigned)(64 * r), oa);
                     }
                 }
                 f = fn;
