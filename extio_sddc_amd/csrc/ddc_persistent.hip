@@ -100,15 +100,15 @@ __device__ __forceinline__ void table_twiddle(float2 *a, const float2 *tbl, int 
     }
 }
 
-// d >= 4 (N = 256, 128, 64): the N-point inverse as mixed-radix Stockham passes on the lanes of
-// wave 0, radix schedule 4-4-4-4, 8-4-4, 4-4-4.  The pass of radix R after a span Ns runs on
+// d = 3..6 (N = 512, 256, 128, 64): the N-point inverse as mixed-radix Stockham passes on the
+// lanes of wave 0, radix schedule 8-8-8, 4-4-4-4, 8-4-4, 4-4-4.  The pass of radix R after a span Ns runs on
 // threads j < N / R: reads elements j + (N / R) r, twiddles W_{R Ns}^{-k r} (k = j mod Ns),
 // inverse DFT-R, writes (j / Ns) R Ns + k + Ns r; the last pass leaves y[j + (N / 4) r] in
-// registers.  LDS element e sits at e ^ ((e >> s) & 31) (s = 1 at N = 64, else 2): conflict-
+// registers.  LDS element e sits at e ^ ((e >> s) & 31) (s = 3, 2, 2, 1): conflict-
 // free for every read and write pattern (tools/r4_tail_model.py, which also checks the passes
 // against numpy).  The [N/16, 16] form it replaces kept 16 lanes busy (d = 4) or fewer; its two
 // passes cost 8-11 % of the launch at d = 4..6 (timing-only build, profiles/r03/ab).
-template <int N> constexpr int tail_radix(int p) { return (N == 128 && p == 0) ? 8 : 4; }
+template <int N> constexpr int tail_radix(int p) { return N == 512 || (N == 128 && p == 0) ? 8 : 4; }
 template <int N> constexpr int tail_passes() { return N == 256 ? 4 : 3; }
 template <int N> constexpr int tail_ns(int p)
 {
@@ -123,7 +123,7 @@ template <int N> constexpr int tail_twoff(int p)   // first twiddle of pass p in
     return o;
 }
 template <int N> constexpr int tail_twn() { return tail_twoff<N>(tail_passes<N>()); }
-template <int N> __device__ __forceinline__ int tail_swz(int e) { return e ^ ((e >> (N == 64 ? 1 : 2)) & 31); }
+template <int N> __device__ __forceinline__ int tail_swz(int e) { return e ^ ((e >> (N == 64 ? 1 : N == 512 ? 3 : 2)) & 31); }
 
 // the forward twiddle W_{R Ns}^{k r} of entry e of the tail's table
 template <int N> __device__ __forceinline__ float2 tail_twiddle(const float2 *__restrict__ tw4096, int e)
@@ -133,6 +133,24 @@ template <int N> __device__ __forceinline__ float2 tail_twiddle(const float2 *__
     const int ns = tail_ns<N>(p), R = tail_radix<N>(p);
     const int o = e - tail_twoff<N>(p), r = o / ns + 1, kk = o % ns;
     return tw4096[(kk * r * (HALF / (R * ns))) & (HALF - 1)];
+}
+
+// the kept outputs of the last pass, u[r] = y[t + (N / R) r]: y[0, 3N/4) (k >= 1), y[N/4, 3N/4) (k = 0)
+template <int N, bool NCO, bool CS16>
+__device__ __forceinline__ void tail_emit(void *__restrict__ out, int fbase, int k, int t, const float2 (&u)[8],
+                                          const OutArgs &oa, const NcoArgs &nco)
+{
+    constexpr int R = tail_radix<N>(tail_passes<N>() - 1), T = N / R;
+    if (t < T) {
+        const __amdgpu_buffer_rsrc_t ro = buf_rsrc(static_cast<char *>(out) + (size_t)fbase * out_bytes<CS16>());
+#pragma unroll
+        for (int r = 0; r < 3 * R / 4; r++) {
+            if (r < R / 4 && k == 0) continue;
+            float2 v = flip(u[r], oa.lsbmask);
+            if constexpr (NCO) v = nco_mix(v, nco, fbase + t + T * r);
+            store_iq<CS16>(v, ro, (unsigned)t, (unsigned)(T * r), oa);
+        }
+    }
 }
 
 template <int N, int P>
@@ -214,7 +232,7 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
 #ifndef SDDC_P_R4TAIL
 #define SDDC_P_R4TAIL 1
 #endif
-    constexpr bool R4T = SDDC_P_R4TAIL && N <= 256;
+    constexpr bool R4T = SDDC_P_R4TAIL && (N <= 256 || N == 512);
     constexpr int TWQ = R4T ? tail_twn<N>() : 15 * SQ;
     __shared__ __attribute__((aligned(16))) float2 twl[15 * 16 + TWQ];
     float2 *const w0 = lds, *const w1 = lds;   // the pass buffers (one 32 KB frame buffer)
@@ -416,6 +434,25 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
                     const float2 zc = *reinterpret_cast<const float2 *>(w0b + ((sc0b - 8u * (unsigned)sh) & (8u * HALF - 8u)));
                     a[r] = split_pq(zk, zc, buf_load16(rpq, tb16, 16u * NT * r));
                 }
+                if constexpr (N == 512 && R4T) {
+                    // d = 3: the 512 filtered bins (inverse input m = t + 256 r) go to LDS, and wave 0
+                    // runs the inverse as three radix-8 Stockham passes (tail_pass) instead of the
+                    // radix-2 pass on every thread and two radix-16 passes on 32 lanes
+                    __syncthreads();   // every wave's Z reads are done
+#pragma unroll
+                    for (int r = 0; r < R0; r++) w1[tail_swz<N>(t + NT * r)] = a[r];
+                    __syncthreads();
+                    if (t < 64) {
+                        float2 v8[8];
+                        const float2 *twq = twl + 15 * 16;
+                        tail_pass<N, 0>(w1, twq, t, v8);
+                        tail_pass<N, 1>(w1, twq, t, v8);
+                        tail_pass<N, 2>(w1, twq, t, v8);
+                        tail_emit<N, NCO, CS16>(out, oblk + emit_base<N>(kc), kc, t, v8, oa, nco);
+                    }
+                    f = fn;
+                    continue;
+                }
                 if constexpr (R0 == 16) dft16<+1>(a, u);
                 else dft<R0, +1>(a, u);
             }
@@ -442,8 +479,13 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
 #pragma unroll
                     for (int r = 0; r < 16; r++) a[r] = LX(w1, t, NB * r);
                 }
+#ifdef SDDC_FAKE_TAIL2   // timing only: no arithmetic in inverse passes 1, 2 (wrong results)
+#pragma unroll
+                for (int r = 0; r < 16; r++) u[r] = a[r];
+#else
                 table_twiddle<+1, TW_EARLY>(a, twl + 15 * 16, R0, t % R0);
                 dft16<+1>(a, u);
+#endif
             }
             if constexpr (WINV) wave_lds_sync();
             else __syncthreads();
@@ -472,8 +514,13 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
 #pragma unroll
                     for (int r = 0; r < 16; r++) a[r] = LX(w0, t, NB * r);
                 }
-                    twiddle_rec16<+1>(a, iw1, iw4);
+#ifdef SDDC_FAKE_TAIL2
+#pragma unroll
+                for (int r = 0; r < 16; r++) u[r] = a[r];
+#else
+                twiddle_rec16<+1>(a, iw1, iw4);
                 dft16<+1>(a, u);
+#endif
                 emit_frame<NB, NCO, CS16>(out, oblk + emit_base<N>(kc), kc, t, u, oa, nco);
             }
         } else {
@@ -495,19 +542,7 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
                     tail_pass<N, 1>(sb, twq, t, u);
                     tail_pass<N, 2>(sb, twq, t, u);
                     if constexpr (tail_passes<N>() == 4) tail_pass<N, 3>(sb, twq, t, u);
-                    // u[r] = y[t + (N / 4) r]; kept: y[0, 3N/4) (k >= 1), y[N/4, 3N/4) (k = 0)
-                    constexpr int TL = N / 4;
-                    if (t < TL) {
-                        const int fbase = oblk + emit_base<N>(kc);
-                        const __amdgpu_buffer_rsrc_t ro = buf_rsrc(static_cast<char *>(out) + (size_t)fbase * out_bytes<CS16>());
-#pragma unroll
-                        for (int r = 0; r < 3; r++) {
-                            if (r == 0 && kc == 0) continue;
-                            float2 vv = flip(u[r], oa.lsbmask);
-                            if constexpr (NCO) vv = nco_mix(vv, nco, fbase + t + TL * r);
-                            store_iq<CS16>(vv, ro, (unsigned)t, (unsigned)(TL * r), oa);
-                        }
-                    }
+                    tail_emit<N, NCO, CS16>(out, oblk + emit_base<N>(kc), kc, t, u, oa, nco);
                 }
                 f = fn;
                 continue;

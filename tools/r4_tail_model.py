@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """numpy model of the d >= 4 inverse tails of r2iq_persistent_kernel (ddc_persistent.hip,
-stockham_tail): the N-point inverse DFT (N = 256, 128, 64 at d = 4, 5, 6) as mixed-radix
-Stockham passes on the lanes of wave 0 (radix schedule 4-4-4-4, 8-4-4 and 4-4-4).  In the pass
+stockham_tail): the N-point inverse DFT (N = 512, 256, 128, 64 at d = 3..6) as mixed-radix
+Stockham passes on the lanes of wave 0 (radix schedule 8-8-8, 4-4-4-4, 8-4-4 and 4-4-4).  In the pass
 of radix R after a span Ns, thread j < N / R reads elements j + (N / R) r, multiplies them by
 e^{+2 pi i k r / (R Ns)} (k = j mod Ns), runs the inverse DFT-R and writes (j / Ns) R Ns + k + Ns r;
 the last pass leaves y[j + (N / R) r] in registers.  Checked against numpy's inverse FFT, plus a
@@ -10,7 +10,7 @@ conflicts of every read and write pattern per 32-lane half of a ds_*_b64 (elemen
 """
 import numpy as np
 
-SCHED = {256: (4, 4, 4, 4), 128: (8, 4, 4), 64: (4, 4, 4)}
+SCHED = {512: (8, 8, 8), 256: (4, 4, 4, 4), 128: (8, 4, 4), 64: (4, 4, 4)}
 
 
 def passes(N):
@@ -67,11 +67,11 @@ def conflicts(A, N):
 
 if __name__ == "__main__":
     rng = np.random.default_rng(1)
-    for N in (256, 128, 64):
+    for N in (512, 256, 128, 64):
         x = rng.standard_normal(N) + 1j * rng.standard_normal(N)
         ref = np.fft.ifft(x) * N
         best = []
-        for a in range(1, 8):
+        for a in range(1, 9):
             for b in range(0, 6):
                 for m in (1, 3, 7, 15, 31):
                     A = lambda e, a=a, b=b, m=m: e ^ (((e >> a) & m) << b)
