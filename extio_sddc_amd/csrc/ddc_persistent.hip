@@ -153,6 +153,36 @@ __device__ __forceinline__ void tail_emit(void *__restrict__ out, int fbase, int
     }
 }
 
+// d = 2 (N = 1024): the inverse as five radix-4 Stockham passes on all 256 threads (the first
+// from the split's registers, m = t + 256 r), ping-pong between two 8 KB regions of the frame
+// buffer with one barrier per pass, instead of a radix-4 pass on every thread and two radix-16
+// passes on wave 0 (which left three waves waiting at the next frame's first barrier).  The
+// twiddles of the pass after a span Ns are W_{4 Ns}^{k r} = w^r with w = W_{4 Ns}^k from an LDS
+// table of 4 + 16 + 64 + 256 entries.  Element e at e ^ ((e >> 2) & 31) in either region:
+// conflict-free (tools/r4_tail_model.py, stockham_wg).
+__device__ __forceinline__ int wg_swz(int e) { return e ^ ((e >> 2) & 31); }
+constexpr int wg_twoff(int ns) { return ns == 4 ? 0 : ns == 16 ? 4 : ns == 64 ? 20 : 84; }
+constexpr int kWgTwN = 340;
+template <int NS, bool LAST>
+__device__ __forceinline__ void wg_pass(const float2 *src, float2 *dst, const float2 *twq, int t, float2 (&u)[4])
+{
+    float2 a[4];
+#pragma unroll
+    for (int r = 0; r < 4; r++) a[r] = src[wg_swz(t + 256 * r)];
+    const int kk = t & (NS - 1);
+    const float2 w1 = twq[wg_twoff(NS) + kk];
+    const float2 w2 = cmul(w1, w1), w3 = cmul(w2, w1);
+    a[1] = TW<+1>(a[1], w1);
+    a[2] = TW<+1>(a[2], w2);
+    a[3] = TW<+1>(a[3], w3);
+    dft4<+1>(a, u);
+    if constexpr (!LAST) {
+#pragma unroll
+        for (int r = 0; r < 4; r++) dst[wg_swz((t / NS) * 4 * NS + kk + NS * r)] = u[r];
+        __syncthreads();
+    }
+}
+
 template <int N, int P>
 __device__ __forceinline__ void tail_pass(float2 *sb, const float2 *twq, int t, float2 (&u)[8])
 {
@@ -233,7 +263,11 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
 #define SDDC_P_R4TAIL 1
 #endif
     constexpr bool R4T = SDDC_P_R4TAIL && (N <= 256 || N == 512);
-    constexpr int TWQ = R4T ? tail_twn<N>() : 15 * SQ;
+#ifndef SDDC_P_WGT
+#define SDDC_P_WGT 1
+#endif
+    constexpr bool WGT = SDDC_P_WGT && N == 1024;
+    constexpr int TWQ = R4T ? tail_twn<N>() : WGT ? kWgTwN : 15 * SQ;
     __shared__ __attribute__((aligned(16))) float2 twl[15 * 16 + TWQ];
     float2 *const w0 = lds, *const w1 = lds;   // the pass buffers (one 32 KB frame buffer)
     // d >= 2: the inverse's last passes run on one wave (N/16 <= 64 butterflies), so they are
@@ -297,10 +331,14 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
         }
     }
     for (int i = tid; i < 15 * 16 + TWQ; i += NT) {
-        if (!R4T || i < 15 * 16) {
+        if ((!R4T && !WGT) || i < 15 * 16) {
             twl[i] = i < 15 * 16 ? tw_p1[i] : tw_q1[i - 15 * 16];   // visible after the first frame's pass-0 barrier
-        } else {
-            if constexpr (R4T) twl[i] = tail_twiddle<N>(tw4096, i - 15 * 16);
+        } else if constexpr (R4T) {
+            twl[i] = tail_twiddle<N>(tw4096, i - 15 * 16);
+        } else if constexpr (WGT) {
+            const int e = i - 15 * 16;   // W_{4 Ns}^k, Ns = 4, 16, 64, 256
+            const int ns = e < 4 ? 4 : e < 20 ? 16 : e < 84 ? 64 : 256;
+            twl[i] = tw4096[((e - wg_twoff(ns)) * (HALF / (4 * ns))) & (HALF - 1)];
         }
     }
 
@@ -433,6 +471,32 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
                     else zk = *reinterpret_cast<const float2 *>(w0b + ((sb0b + 8u * (unsigned)sh) & (8u * HALF - 8u)));
                     const float2 zc = *reinterpret_cast<const float2 *>(w0b + ((sc0b - 8u * (unsigned)sh) & (8u * HALF - 8u)));
                     a[r] = split_pq(zk, zc, buf_load16(rpq, tb16, 16u * NT * r));
+                }
+                if constexpr (WGT) {
+                    float2 u4[4];
+                    dft4<+1>(a, u4);   // pass 0 (Ns = 1)
+                    __syncthreads();   // every wave's Z reads are done
+                    float2 *const ra = w1, *const rb = w1 + 1024;
+#pragma unroll
+                    for (int r = 0; r < 4; r++) ra[wg_swz(4 * t + r)] = u4[r];
+                    __syncthreads();
+                    const float2 *twq = twl + 15 * 16;
+                    wg_pass<4, false>(ra, rb, twq, t, u4);
+                    wg_pass<16, false>(rb, ra, twq, t, u4);
+                    wg_pass<64, false>(ra, rb, twq, t, u4);
+                    wg_pass<256, true>(rb, ra, twq, t, u4);
+                    // u4[r] = y[t + 256 r]; kept: y[0, 768) (k >= 1), y[256, 768) (k = 0)
+                    const int fbase = oblk + emit_base<N>(kc);
+                    const __amdgpu_buffer_rsrc_t ro = buf_rsrc(static_cast<char *>(out) + (size_t)fbase * out_bytes<CS16>());
+#pragma unroll
+                    for (int r = 0; r < 3; r++) {
+                        if (r == 0 && kc == 0) continue;
+                        float2 vv = flip(u4[r], oa.lsbmask);
+                        if constexpr (NCO) vv = nco_mix(vv, nco, fbase + t + 256 * r);
+                        store_iq<CS16>(vv, ro, (unsigned)t, (unsigned)(256 * r), oa);
+                    }
+                    f = fn;
+                    continue;
                 }
                 if constexpr (N == 512 && R4T) {
                     // d = 3: the 512 filtered bins (inverse input m = t + 256 r) go to LDS, and wave 0

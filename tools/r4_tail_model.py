@@ -85,3 +85,75 @@ if __name__ == "__main__":
         err = np.abs(stockham_inv(x, N, A) - ref).max() / np.abs(ref).max()
         print(f"N={N} schedule {SCHED[N]}: rel err {err:.1e}; plain layout conflicts {conflicts(lambda e: e, N)}, "
               f"best swizzle e ^ (((e >> {a}) & {m}) << {b}): worst {w}-way, {t} extra cycles")
+
+
+def stockham_wg(x, N, A=lambda e: e):
+    """d = 1, 2 (N = 2048, 1024): radix N/256 from registers (m = t + 256 r) then four radix-4
+    passes on all 256 threads (N/1024 butterflies per thread), ping-pong between two regions."""
+    R0 = N // 256
+    bufs = [np.zeros(N, complex), np.zeros(N, complex)]
+    # pass 0: thread t holds m = t + 256 r
+    for t in range(256):
+        a = np.array([x[t + 256 * r] for r in range(R0)])
+        u = np.fft.ifft(a) * R0
+        for r in range(R0):
+            bufs[0][A(R0 * t + r)] = u[r]
+    ns, src = R0, 0
+    y = np.zeros(N, complex)
+    for p in range(4):
+        T = N // 4
+        for j in range(T):
+            k = j % ns
+            a = np.array([bufs[src][A(j + T * r)] for r in range(4)])
+            a = a * np.exp(2j * np.pi * k * np.arange(4) / (4 * ns))
+            u = np.fft.ifft(a) * 4
+            for r in range(4):
+                if p < 3:
+                    bufs[1 - src][A((j // ns) * 4 * ns + k + ns * r)] = u[r]
+                else:
+                    y[j + T * r] = u[r]
+        ns *= 4
+        src = 1 - src
+    return y
+
+
+def conflicts_wg(A, N):
+    R0 = N // 256
+    T = N // 4
+    pats = [[[R0 * t + r for t in range(256)] for r in range(R0)]]
+    ns = R0
+    for p in range(4):
+        pats.append([[j + T * r for j in range(T)] for r in range(4)])
+        if p < 3:
+            pats.append([[(j // ns) * 4 * ns + j % ns + ns * r for j in range(T)] for r in range(4)])
+        ns *= 4
+    tot, worst = 0, 1
+    for pat in pats:
+        for lanes in pat:
+            for h in range(0, len(lanes), 32):
+                sl = [A(e) % 32 for e in lanes[h:h + 32]]
+                c = max(np.bincount(sl, minlength=32))
+                tot += c - 1
+                worst = max(worst, c)
+    return worst, tot
+
+
+if __name__ == "__main__":
+    rng = np.random.default_rng(2)
+    for N in (1024, 2048):
+        x = rng.standard_normal(N) + 1j * rng.standard_normal(N)
+        ref = np.fft.ifft(x) * N
+        best = []
+        for a in range(1, 10):
+            for m in (1, 3, 7, 15, 31):
+                A = lambda e, a=a, m=m: e ^ ((e >> a) & m)
+                if sorted(A(e) for e in range(N)) != list(range(N)):
+                    continue
+                w, t = conflicts_wg(A, N)
+                best.append((w, t, a, m))
+        best.sort()
+        w, t, a, m = best[0]
+        A = lambda e: e ^ ((e >> a) & m)
+        err = np.abs(stockham_wg(x, N, A) - ref).max() / np.abs(ref).max()
+        print(f"N={N} workgroup schedule {N // 256}-4-4-4-4: rel err {err:.1e}; plain {conflicts_wg(lambda e: e, N)}, "
+              f"best swizzle e ^ ((e >> {a}) & {m}): worst {w}-way, {t} extra")
