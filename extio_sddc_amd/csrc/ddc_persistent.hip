@@ -153,32 +153,46 @@ __device__ __forceinline__ void tail_emit(void *__restrict__ out, int fbase, int
     }
 }
 
-// d = 2 (N = 1024): the inverse as five radix-4 Stockham passes on all 256 threads (the first
-// from the split's registers, m = t + 256 r), ping-pong between two 8 KB regions of the frame
-// buffer with one barrier per pass, instead of a radix-4 pass on every thread and two radix-16
-// passes on wave 0 (which left three waves waiting at the next frame's first barrier).  The
+// d = 2 (N = 1024; N = 2048 with SDDC_P_WGT=2): the inverse as a radix-N/256 pass from the split's registers
+// (m = t + 256 r) and four radix-4 Stockham passes on all 256 threads (N / 1024 butterflies per
+// thread), ping-pong between two regions of the frame buffer with one barrier per pass, instead
+// of radix-16 passes on 2 waves (d = 1) or wave 0 (d = 2) while the other waves wait.  The
 // twiddles of the pass after a span Ns are W_{4 Ns}^{k r} = w^r with w = W_{4 Ns}^k from an LDS
-// table of 4 + 16 + 64 + 256 entries.  Element e at e ^ ((e >> 2) & 31) in either region:
-// conflict-free (tools/r4_tail_model.py, stockham_wg).
-__device__ __forceinline__ int wg_swz(int e) { return e ^ ((e >> 2) & 31); }
-constexpr int wg_twoff(int ns) { return ns == 4 ? 0 : ns == 16 ? 4 : ns == 64 ? 20 : 84; }
-constexpr int kWgTwN = 340;
-template <int NS, bool LAST>
-__device__ __forceinline__ void wg_pass(const float2 *src, float2 *dst, const float2 *twq, int t, float2 (&u)[4])
+// table of (N - N/256) / 3 entries.  Element e at wg_swz(e) in either region: conflict-free
+// (tools/r4_tail_model.py, stockham_wg).
+template <int N> __device__ __forceinline__ int wg_swz(int e)
 {
-    float2 a[4];
+    if constexpr (N == 2048) return e ^ ((e >> 2) & 31) ^ ((e >> 5) & 7);
+    else return e ^ ((e >> 2) & 31);
+}
+template <int N> constexpr int wg_twoff(int ns) { return (ns - N / 256) / 3; }
+template <int N> constexpr int wg_twn() { return (N - N / 256) / 3; }
+template <int N, int NS, bool LAST>
+__device__ __forceinline__ void wg_pass(const float2 *src, float2 *dst, const float2 *twq, int t,
+                                        float2 (&u)[N / 1024][4])
+{
+    constexpr int B = N / 1024, T = N / 4;
 #pragma unroll
-    for (int r = 0; r < 4; r++) a[r] = src[wg_swz(t + 256 * r)];
-    const int kk = t & (NS - 1);
-    const float2 w1 = twq[wg_twoff(NS) + kk];
-    const float2 w2 = cmul(w1, w1), w3 = cmul(w2, w1);
-    a[1] = TW<+1>(a[1], w1);
-    a[2] = TW<+1>(a[2], w2);
-    a[3] = TW<+1>(a[3], w3);
-    dft4<+1>(a, u);
+    for (int b = 0; b < B; b++) {
+        const int j = t + 256 * b;
+        float2 a[4];
+#pragma unroll
+        for (int r = 0; r < 4; r++) a[r] = src[wg_swz<N>(j + T * r)];
+        const int kk = j & (NS - 1);
+        const float2 w1 = twq[wg_twoff<N>(NS) + kk];
+        const float2 w2 = cmul(w1, w1), w3 = cmul(w2, w1);
+        a[1] = TW<+1>(a[1], w1);
+        a[2] = TW<+1>(a[2], w2);
+        a[3] = TW<+1>(a[3], w3);
+        dft4<+1>(a, u[b]);
+    }
     if constexpr (!LAST) {
 #pragma unroll
-        for (int r = 0; r < 4; r++) dst[wg_swz((t / NS) * 4 * NS + kk + NS * r)] = u[r];
+        for (int b = 0; b < B; b++) {
+            const int j = t + 256 * b, kk = j & (NS - 1);
+#pragma unroll
+            for (int r = 0; r < 4; r++) dst[wg_swz<N>((j / NS) * 4 * NS + kk + NS * r)] = u[b][r];
+        }
         __syncthreads();
     }
 }
@@ -266,8 +280,10 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
 #ifndef SDDC_P_WGT
 #define SDDC_P_WGT 1
 #endif
-    constexpr bool WGT = SDDC_P_WGT && N == 1024;
-    constexpr int TWQ = R4T ? tail_twn<N>() : WGT ? kWgTwN : 15 * SQ;
+    // d = 2 only: at d = 1 (N = 2048, two butterflies per thread per pass) the same form measured
+    // 7-8 % slower than the two-wave radix-16 tail (profiles/r03/ab/d12_wg.txt)
+    constexpr bool WGT = SDDC_P_WGT && (N == 1024 || (SDDC_P_WGT > 1 && N == 2048));
+    constexpr int TWQ = R4T ? tail_twn<N>() : WGT ? wg_twn<N>() : 15 * SQ;
     __shared__ __attribute__((aligned(16))) float2 twl[15 * 16 + TWQ];
     float2 *const w0 = lds, *const w1 = lds;   // the pass buffers (one 32 KB frame buffer)
     // d >= 2: the inverse's last passes run on one wave (N/16 <= 64 butterflies), so they are
@@ -336,9 +352,11 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
         } else if constexpr (R4T) {
             twl[i] = tail_twiddle<N>(tw4096, i - 15 * 16);
         } else if constexpr (WGT) {
-            const int e = i - 15 * 16;   // W_{4 Ns}^k, Ns = 4, 16, 64, 256
-            const int ns = e < 4 ? 4 : e < 20 ? 16 : e < 84 ? 64 : 256;
-            twl[i] = tw4096[((e - wg_twoff(ns)) * (HALF / (4 * ns))) & (HALF - 1)];
+            const int e = i - 15 * 16;   // W_{4 Ns}^k, Ns = N/256 x 1, 4, 16, 64
+            constexpr int r0 = N / 256;
+            const int ns = e < wg_twoff<N>(4 * r0) ? r0 : e < wg_twoff<N>(16 * r0) ? 4 * r0
+                         : e < wg_twoff<N>(64 * r0) ? 16 * r0 : 64 * r0;
+            twl[i] = tw4096[((e - wg_twoff<N>(ns)) * (HALF / (4 * ns))) & (HALF - 1)];
         }
     }
 
@@ -473,27 +491,36 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
                     a[r] = split_pq(zk, zc, buf_load16(rpq, tb16, 16u * NT * r));
                 }
                 if constexpr (WGT) {
-                    float2 u4[4];
-                    dft4<+1>(a, u4);   // pass 0 (Ns = 1)
-                    __syncthreads();   // every wave's Z reads are done
-                    float2 *const ra = w1, *const rb = w1 + 1024;
+                    constexpr int B = N / 1024, T = N / 4;
+                    {
+                        float2 u0[R0];
+                        if constexpr (R0 == 8) dft8<+1>(a, u0);   // pass 0 (Ns = 1)
+                        else dft4<+1>(a, u0);
+                        __syncthreads();   // every wave's Z reads are done
 #pragma unroll
-                    for (int r = 0; r < 4; r++) ra[wg_swz(4 * t + r)] = u4[r];
+                        for (int r = 0; r < R0; r++) w1[wg_swz<N>(R0 * t + r)] = u0[r];
+                    }
                     __syncthreads();
+                    float2 *const ra = w1, *const rb = w1 + N;
                     const float2 *twq = twl + 15 * 16;
-                    wg_pass<4, false>(ra, rb, twq, t, u4);
-                    wg_pass<16, false>(rb, ra, twq, t, u4);
-                    wg_pass<64, false>(ra, rb, twq, t, u4);
-                    wg_pass<256, true>(rb, ra, twq, t, u4);
-                    // u4[r] = y[t + 256 r]; kept: y[0, 768) (k >= 1), y[256, 768) (k = 0)
+                    float2 u4[B][4];
+                    wg_pass<N, R0, false>(ra, rb, twq, t, u4);
+                    wg_pass<N, 4 * R0, false>(rb, ra, twq, t, u4);
+                    wg_pass<N, 16 * R0, false>(ra, rb, twq, t, u4);
+                    wg_pass<N, 64 * R0, true>(rb, ra, twq, t, u4);
+                    // u4[b][r] = y[t + 256 b + (N/4) r]; kept: y[0, 3N/4) (k >= 1), y[N/4, 3N/4) (k = 0)
                     const int fbase = oblk + emit_base<N>(kc);
                     const __amdgpu_buffer_rsrc_t ro = buf_rsrc(static_cast<char *>(out) + (size_t)fbase * out_bytes<CS16>());
 #pragma unroll
                     for (int r = 0; r < 3; r++) {
                         if (r == 0 && kc == 0) continue;
-                        float2 vv = flip(u4[r], oa.lsbmask);
-                        if constexpr (NCO) vv = nco_mix(vv, nco, fbase + t + 256 * r);
-                        store_iq<CS16>(vv, ro, (unsigned)t, (unsigned)(256 * r), oa);
+#pragma unroll
+                        for (int b = 0; b < B; b++) {
+                            const int n = t + 256 * b + T * r;
+                            float2 vv = flip(u4[b][r], oa.lsbmask);
+                            if constexpr (NCO) vv = nco_mix(vv, nco, fbase + n);
+                            store_iq<CS16>(vv, ro, (unsigned)t, (unsigned)(256 * b + T * r), oa);
+                        }
                     }
                     f = fn;
                     continue;

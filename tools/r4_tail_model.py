@@ -157,3 +157,17 @@ if __name__ == "__main__":
         err = np.abs(stockham_wg(x, N, A) - ref).max() / np.abs(ref).max()
         print(f"N={N} workgroup schedule {N // 256}-4-4-4-4: rel err {err:.1e}; plain {conflicts_wg(lambda e: e, N)}, "
               f"best swizzle e ^ ((e >> {a}) & {m}): worst {w}-way, {t} extra")
+    # N = 2048: a wider search (two XOR terms)
+    N = 2048
+    best = []
+    for a in range(1, 10):
+        for m in (7, 15, 31):
+            for a2 in range(a + 1, 11):
+                for m2 in (1, 3, 7, 15, 31):
+                    A = lambda e, a=a, m=m, a2=a2, m2=m2: e ^ ((e >> a) & m) ^ ((e >> a2) & m2)
+                    if sorted(A(e) for e in range(N)) != list(range(N)):
+                        continue
+                    w, t = conflicts_wg(A, N)
+                    best.append((w, t, a, m, a2, m2))
+    best.sort()
+    print("N=2048 two-term swizzles:", best[:3])
