@@ -307,7 +307,10 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
 #ifndef SDDC_P_QUEUE
 #define SDDC_P_QUEUE 1
 #endif
-    constexpr bool PQ = SDDC_P_QUEUE && D <= 2;
+#ifndef SDDC_P_QUEUE_DMAX   // re-measured after the d >= 3 tail rewrite: still 2-14 % slower at d = 3..6
+#define SDDC_P_QUEUE_DMAX 2   // (profiles/r03/ab/p_queue_d3_6_after_tails.txt)
+#endif
+    constexpr bool PQ = SDDC_P_QUEUE && D <= SDDC_P_QUEUE_DMAX;
     __shared__ int s_first, s_next;
     constexpr int QLANE = 64 * 3;
     const bool qw = __builtin_amdgcn_readfirstlane(tid >> 6) == 3;
