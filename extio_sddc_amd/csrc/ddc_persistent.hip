@@ -316,16 +316,27 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
     const bool qw = __builtin_amdgcn_readfirstlane(tid >> 6) == 3;
     const int f1s = (int)(((long long)nframes * (w + 1)) / G);   // the static split's range end
     FsQueue q;
-    if constexpr (PQ) q.init(wq, nframes, w & (FS_SHARDS - 1));
+#ifndef SDDC_P_SFIRST
+#define SDDC_P_SFIRST 1
+#endif
+    // the first two frames static (fs_static_frame): no atomic round trip before the first frame
+    constexpr int PSTAT = SDDC_P_SFIRST ? 2 : 0;
+    if constexpr (PQ) q.init(wq, nframes, w & (FS_SHARDS - 1), PSTAT ? G : 0, PSTAT ? PSTAT : 1);
     if (qw) {
         int g0, g1;
         if constexpr (PQ) {
-            q.take();
-            q.peek();
-            g0 = q.resolve();
-            q.take();
-            q.peek();
-            g1 = q.resolve();
+            g0 = PSTAT ? fs_static_frame(nframes, G, w, 0, PSTAT) : -1;
+            g1 = PSTAT ? fs_static_frame(nframes, G, w, 1, PSTAT) : -1;
+            if (g0 < 0) {   // no static frames (small batches): both from the queue
+                q.take();
+                q.peek();
+                g0 = q.resolve();
+            }
+            if (g1 < 0) {
+                q.take();
+                q.peek();
+                g1 = g0 >= 0 ? q.resolve() : -1;
+            }
             q.take();
         } else {
             const int f0 = (int)(((long long)nframes * w) / G);

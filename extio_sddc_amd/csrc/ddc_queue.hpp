@@ -44,31 +44,37 @@ constexpr unsigned FS_OOB = 0x80000000u;   // a buffer offset past the queue slo
 // homed there) frames of shard s go to its home workgroups in blockIdx order (frame lo_s + blockIdx
 // / 8), and the shard's tickets count from there.  The first frame's input then loads at once,
 // with no device-scope atomic round trip in front of it (grid = 0: every frame from the queue).
-__device__ __forceinline__ int fs_shard_pre(int nframes, int grid, int s)
+// per: static frames per workgroup (the persistent kernel's d = 1, 2 queue takes two, its first
+// and its second frame, so neither waits for an atomic).
+__device__ __forceinline__ int fs_shard_nwg(int grid, int s) { return (grid - s + FS_SHARDS - 1) / FS_SHARDS; }
+__device__ __forceinline__ int fs_shard_pre(int nframes, int grid, int s, int per)
 {
     const int cnt = fs_shard_lo(nframes, s + 1) - fs_shard_lo(nframes, s);
-    const int nwg = (grid - s + FS_SHARDS - 1) / FS_SHARDS;
-    return cnt < nwg ? cnt : nwg;
+    const int n = per * fs_shard_nwg(grid, s);
+    return cnt < n ? cnt : n;
 }
-__device__ __forceinline__ int fs_static_first(int nframes, int grid, int w)
+// static frame i (< per) of workgroup w: frame lo_s + i nwg_s + blockIdx / 8 of its home shard s
+__device__ __forceinline__ int fs_static_frame(int nframes, int grid, int w, int i, int per)
 {
-    const int s = w & (FS_SHARDS - 1), j = w / FS_SHARDS;
-    return j < fs_shard_pre(nframes, grid, s) ? fs_shard_lo(nframes, s) + j : -1;
+    const int s = w & (FS_SHARDS - 1), e = i * fs_shard_nwg(grid, s) + w / FS_SHARDS;
+    return e < fs_shard_pre(nframes, grid, s, per) ? fs_shard_lo(nframes, s) + e : -1;
 }
+__device__ __forceinline__ int fs_static_first(int nframes, int grid, int w) { return fs_static_frame(nframes, grid, w, 0, 1); }
 struct FsQueue {
     __amdgpu_buffer_rsrc_t rq;   // the queue slot as a buffer (kFsQueueWords words)
-    int nframes, sh0, grid;
+    int nframes, sh0, grid, per;
     int shn;        // shard of the pending ticket (8: every shard dry)
     int lo, cnt;    // first frame and size of that shard (cnt = 0 once every shard is dry)
     int tk;         // lane 0: the pending ticket
     int pv;         // its value, read by peek()
 
-    __device__ __forceinline__ void init(unsigned *wq, int nframes_, int home, int grid_ = 0)
+    __device__ __forceinline__ void init(unsigned *wq, int nframes_, int home, int grid_ = 0, int per_ = 1)
     {
         rq = __builtin_amdgcn_make_buffer_rsrc(wq, (short)0, 4 * kFsQueueWords, 0x00020000);
         nframes = nframes_;
         sh0 = home;
         grid = grid_;
+        per = per_;
         set_shard(0);
     }
     __device__ __forceinline__ void set_shard(int sh)
@@ -78,7 +84,7 @@ struct FsQueue {
         lo = fs_shard_lo(nframes, s);
         cnt = sh < FS_SHARDS ? fs_shard_lo(nframes, s + 1) - lo : 0;
         if (grid) {   // the static first frames
-            const int pre = fs_shard_pre(nframes, grid, s);
+            const int pre = fs_shard_pre(nframes, grid, s, per);
             lo += pre;
             cnt -= pre;
         }
