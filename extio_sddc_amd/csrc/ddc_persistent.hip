@@ -902,11 +902,17 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
     // home shard: blockIdx % 8, the XCD under round-robin placement.  The first frame is static
     // (fs_static_first): its input loads go out at once, ahead of the table copies, with no device-
     // scope atomic round trip in front of them (+0.4-1.7 %, profiles/r03/ab/fs_static_first*.txt)
-    q.init(wq, nframes, w & (FS_SHARDS - 1), (int)gridDim.x);
+#ifndef SDDC_FS_SPER
+#define SDDC_FS_SPER 1   // static frames per workgroup; 2 (frame 0 resolves no ticket) measured 1.7 % slower
+                         // (profiles/r03/ab/fs_two_static_frames.txt)
+#endif
+    q.init(wq, nframes, w & (FS_SHARDS - 1), (int)gridDim.x, SDDC_FS_SPER);
 #ifdef SDDC_FS_QSTATIC
     const int f_stat = -1;
+    const int f_stat1 = -1;
 #else
-    const int f_stat = fs_static_first(nframes, (int)gridDim.x, w);   // wave-uniform; -1: none
+    const int f_stat = fs_static_frame(nframes, (int)gridDim.x, w, 0, SDDC_FS_SPER);   // wave-uniform; -1: none
+    int f_stat1 = SDDC_FS_SPER > 1 && f_stat >= 0 ? fs_static_frame(nframes, (int)gridDim.x, w, 1, SDDC_FS_SPER) : -1;
 #endif
     int x[16];
     if (f_stat >= 0) load_frame(in32, f_stat / FRAMES, f_stat % FRAMES, x);
@@ -946,7 +952,7 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
     FS_STAMP_INIT();
 
     while (f >= 0) {
-        if (qw) FS_QSTAMP(3, q.peek());
+        if (qw && f_stat1 < 0) FS_QSTAMP(3, q.peek());   // (frame 0 with a static second frame: no ticket read)
         int z = 0;
         asm volatile("" : "+s"(z));
         const int t = tid + z;
@@ -1070,11 +1076,19 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
             });
 #else
             int f_n;
-            FS_QSTAMP(0, f_n = q.resolve());
-            FS_QSTAMP(1, if (tid == QLANE) s_next = f_n);
-            FS_QSTAMP(2, q.take());
+            if (f_stat1 >= 0) {   // frame 0: the static second frame; the ticket taken at start waits a frame
+                f_n = f_stat1;
+                if (tid == QLANE) s_next = f_n;
+            } else {
+                FS_QSTAMP(0, f_n = q.resolve());
+                FS_QSTAMP(1, if (tid == QLANE) s_next = f_n);
+                FS_QSTAMP(2, q.take());
+            }
 #endif
         }
+#ifndef SDDC_FS_QSTATIC
+        f_stat1 = -1;
+#endif
         FS_SYNC(5);
         // the next frame's input: issued here rather than in pass 0, so its 16 registers are
         // free through forward pass 2 and the split, and the loads' waits never hold pass 2
