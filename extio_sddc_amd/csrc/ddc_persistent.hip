@@ -1092,12 +1092,22 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
         FS_SYNC(5);
         // the next frame's input: issued here rather than in pass 0, so its 16 registers are
         // free through forward pass 2 and the split, and the loads' waits never hold pass 2
+// the next frame's number (s_next) is read behind inverse pass 1's data reads, so its LDS round
+// trip runs under theirs: +0.4-0.8 % in three interleaved rounds, bit-identical
+// (profiles/r03/ab/fs_late_next_frame_read.txt)
+#ifndef SDDC_FS_LATE_NEXT
+#define SDDC_FS_LATE_NEXT 1
+#endif
+#if !SDDC_FS_LATE_NEXT
         const int fn = s_next;
         if (fn >= 0) {
             blk = fn / FRAMES;
             k = fn - blk * FRAMES;
             load_frame(in32, blk, k, x);
         }
+#else
+        int fn;
+#endif
         // ---- inverse pass 1 (R16, NS16): table twiddles W_256^{-(t%16) r} ----
         // inverse pass 2's bases: W^t, W^{4t} and the lane's modulation factor g_t
         {
@@ -1108,6 +1118,14 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
 #pragma unroll
             for (int r = 0; r < 16; r++)
                 XRD(a[r], *reinterpret_cast<const float2 *>(reinterpret_cast<const char *>(lds) + ((sT8 ^ (8u * r)) + 2048u * r)));
+#if SDDC_FS_LATE_NEXT   // the next frame read behind the pass's data reads (its LDS round trip under theirs)
+            fn = s_next;
+            if (fn >= 0) {
+                blk = fn / FRAMES;
+                k = fn - blk * FRAMES;
+                load_frame(in32, blk, k, x);
+            }
+#endif
             table_twiddle<+1, true>(a, twl, 16, x15);
             dft16<+1>(a, u);
         }
