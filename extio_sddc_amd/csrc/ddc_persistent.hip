@@ -902,6 +902,9 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
     // home shard: blockIdx % 8, the XCD under round-robin placement.  The first frame is static
     // (fs_static_first): its input loads go out at once, ahead of the table copies, with no device-
     // scope atomic round trip in front of them (+0.4-1.7 %, profiles/r03/ab/fs_static_first*.txt)
+#ifndef SDDC_FS_QTOP
+#define SDDC_FS_QTOP 0
+#endif
 #ifndef SDDC_FS_SPER
 #define SDDC_FS_SPER 1   // static frames per workgroup; 2 (frame 0 resolves no ticket) measured 1.7 % slower
                          // (profiles/r03/ab/fs_two_static_frames.txt)
@@ -953,6 +956,15 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
 
     while (f >= 0) {
         if (qw && f_stat1 < 0) FS_QSTAMP(3, q.peek());   // (frame 0 with a static second frame: no ticket read)
+#if SDDC_FS_QTOP && !defined(SDDC_FS_QSTATIC)
+        // the dequeue at the frame top (the ticket was taken a frame ago): the next frame into
+        // s_next (read after barrier 5) and a ticket for the frame after it
+        if (qw && f_stat1 < 0) {
+            const int f_n = q.resolve();
+            if (tid == QLANE) s_next = f_n;
+            q.take();
+        }
+#endif
         int z = 0;
         asm volatile("" : "+s"(z));
         const int t = tid + z;
@@ -1076,7 +1088,9 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
             });
 #else
             int f_n;
-            if (f_stat1 >= 0) {   // frame 0: the static second frame; the ticket taken at start waits a frame
+            if (SDDC_FS_QTOP) {
+                // done at the frame top
+            } else if (f_stat1 >= 0) {   // frame 0: the static second frame; the ticket taken at start waits a frame
                 f_n = f_stat1;
                 if (tid == QLANE) s_next = f_n;
             } else {
