@@ -919,6 +919,15 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
 #endif
     int x[16];
     if (f_stat >= 0) load_frame(in32, f_stat / FRAMES, f_stat % FRAMES, x);
+#ifndef SDDC_FS_QALL
+#define SDDC_FS_QALL 0
+#endif
+    if constexpr (SDDC_FS_QALL) {
+        // every wave runs the dequeue's scalar bookkeeping inside inverse pass 0's DFT (no branch,
+        // so it interleaves with the VALU); only the queue wave's atomics are in range
+        q.mine = qw;
+        if (!qw) q.take();   // a zero ticket (out of range)
+    }
     if (qw) {
 #ifdef SDDC_FS_QSTATIC
         const int f_first = w < nframes ? w : -1;
@@ -955,7 +964,7 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
     FS_STAMP_INIT();
 
     while (f >= 0) {
-        if (qw && f_stat1 < 0) FS_QSTAMP(3, q.peek());   // (frame 0 with a static second frame: no ticket read)
+        if ((qw || SDDC_FS_QALL) && f_stat1 < 0) FS_QSTAMP(3, q.peek());   // (frame 0 with a static second frame: no ticket read)
 #if SDDC_FS_QTOP && !defined(SDDC_FS_QSTATIC)
         // the dequeue at the frame top (the ticket was taken a frame ago): the next frame into
         // s_next (read after barrier 5) and a ticket for the frame after it
@@ -1069,6 +1078,15 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
                     }
                 }
             }
+#if SDDC_FS_QALL && !defined(SDDC_FS_QSTATIC)
+            if (f_stat1 >= 0) {
+                if (tid == QLANE) s_next = f_stat1;
+            } else {
+                const int f_n = q.resolve();
+                if (tid == QLANE) s_next = f_n;
+                q.take();
+            }
+#endif
             dft16<+1>(a, u);
         }
         FS_SYNC(4);   // every wave's pass-2 reads are done
@@ -1088,7 +1106,7 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
             });
 #else
             int f_n;
-            if (SDDC_FS_QTOP) {
+            if (SDDC_FS_QTOP || SDDC_FS_QALL) {
                 // done at the frame top
             } else if (f_stat1 >= 0) {   // frame 0: the static second frame; the ticket taken at start waits a frame
                 f_n = f_stat1;

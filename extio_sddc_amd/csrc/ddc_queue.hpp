@@ -66,6 +66,7 @@ struct FsQueue {
     int shn;        // shard of the pending ticket (8: every shard dry)
     int lo, cnt;    // first frame and size of that shard (cnt = 0 once every shard is dry)
     int tk;         // lane 0: the pending ticket
+    bool mine = true;   // false: a wave that runs the bookkeeping without a queue (its atomics out of range)
     int pv;         // its value, read by peek()
 
     __device__ __forceinline__ void init(unsigned *wq, int nframes_, int home, int grid_ = 0, int per_ = 1)
@@ -95,7 +96,7 @@ struct FsQueue {
     __device__ __forceinline__ void take()
     {
         const unsigned off = shn < FS_SHARDS ? 64u * (unsigned)((sh0 + shn) & (FS_SHARDS - 1)) : FS_OOB;
-        const unsigned voff = (threadIdx.x & 63) == 0 ? off : FS_OOB;
+        const unsigned voff = (threadIdx.x & 63) == 0 && mine ? off : FS_OOB;
         tk = __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(1, rq, voff, 0, 0);
     }
     // reads the pending ticket (waits for its atomic): at the top of a frame, where the wait is
