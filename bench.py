@@ -231,9 +231,11 @@ def reference_equivalent(backend_msps: float, d: int):
     try:
         with open(os.path.join(ROOT, "profiles", "cpu_calibration.json")) as f:
             r = json.load(f)["ratio_reference_over_avx2_backend"][str(d)]
-        return {"value": backend_msps * r, "ratio": r,
-                "basis": "reference AVX2 r2iq (survey probe) / this library's AVX2 backend, both 1 core of the "
-                         "survey container type (tools/cpu_calib.py)"}
+        return {"value": backend_msps * r, "ratio": r, "kind": "cross-CPU estimate",
+                "basis": "reference AVX2 r2iq (survey probe) / this library's AVX2 backend, both measured on 1 core "
+                         "of the survey's Xeon container (tools/cpu_calib.py), applied to this host's CPU: an "
+                         "estimate across CPU types, not a measurement of the reference here (the reference "
+                         "r2iq needs <fftw3.h>, absent from the image); the measured baseline is `value`"}
     except Exception:
         return None
 
@@ -684,7 +686,7 @@ def main() -> None:
             cb["all_cores"] = cpu_baseline_all_cores(d, tb, sample, ns, args.cpu_budget)
         except Exception as e:   # the 1-core figure stands on its own
             cb["all_cores"] = {"error": str(e)}
-        cb["reference_equivalent_estimate"] = reference_equivalent(cb["value"], d)
+        cb["reference_equivalent_cross_cpu_estimate"] = reference_equivalent(cb["value"], d)
         result["cpu_baseline"] = cb
         result["gpu_over_cpu_backend_1core"] = value / cb["value"]
         result["iq_max_rel_err"] = cb.pop("iq_max_rel_err_gpu_vs_oracle_f64")
@@ -700,7 +702,7 @@ def main() -> None:
                 cbd = cpu_baseline(dd, args.tunebin, gout, d_in[: HALF + ns * BLOCK].cpu().numpy(), ns, 2.0, 1.0)
                 line["cpu_backend_1core_MSps"] = cbd["value"]
                 line["cpu_oracle_port_1core_MSps"] = cbd["oracle_f32_port_1core_MSps"]
-                line["cpu_reference_equivalent_MSps"] = (reference_equivalent(cbd["value"], dd) or {}).get("value")
+                line["cpu_reference_equivalent_cross_cpu_estimate_MSps"] = (reference_equivalent(cbd["value"], dd) or {}).get("value")
                 line["iq_max_rel_err"] = cbd["iq_max_rel_err_gpu_vs_oracle_f64"]
         result["sweep"] = sweep
     if rank == 0:

@@ -1,0 +1,462 @@
+// ddc_fs.hip — the d = 0 single-channel kernel for gfx950 (the BASELINE C2 path, decim = 2):
+// the fused-split (FS) frame kernel.
+//
+// Per frame it runs the reference's worker (Core/fft_mt_r2iq_impl.hpp:76-138): convert (+ rand),
+// r2c 8192 as a 4096-point packed complex FFT, split x shift x filter with the zero fill, the
+// inverse 4096-point FFT and the overlap-discard store, as six radix-16 passes on 256 threads
+// (16 points each) with four LDS exchanges:
+//   F0 convert + DFT-16 from registers      -> LDS (padded rows: no address VALU)
+//   F1 table twiddles + DFT-16               -> LDS (XOR-swizzled)
+//   F2 recurrence twiddles + DFT-16, then the split x filter and I0's DFT-16 in registers
+//                                            -> LDS (XOR-keyed rows)
+//   I1 table twiddles + DFT-16               -> LDS (XOR-swizzled)
+//   I2 twiddles g_t W^{-t r} + DFT-16, quarter turns, overlap-discard IQ stores.
+//
+// The fused split.  F2's butterfly on lane l is column c = kFsPerm[l]: it produces Z[c + 256 k],
+// k = 0..15.  The split of bin b needs Z[-b]; for b = c + 256 k that is Z[(256 - c) + 256 (15 - k)],
+// and lane l ^ 1 holds column 256 - c (the permutation pairs the lanes), so the mirror is the
+// partner lane's register 15 - k: a DPP quad_perm [1,0,3,2] operand of the split's FMAs
+// (v_fmac_f32_dpp, no extra instruction).  The self-mirrored columns 0 and 128 (lanes 0, 1 of
+// wave 0) read their own registers instead (a wave-uniform branch, selects in wave 0 only).
+// The inverse then runs on absolute bin indices: I0's butterfly c takes the split values of
+// bins c + 256 s, i.e. the lane's own registers.  The tune shift, which the reference applies as
+// an input offset (T[m] = X[tb + m] H[m], impl.hpp:84-96), becomes the output modulation
+// y[n] = e^{-2 pi i tb n / 4096} y'[n] (y' the inverse FFT over bins):
+//   n = t + 256 k:  e^{-2 pi i tb t / 4096} (lane factor g_t, folded into I2's twiddles)
+//   x W_16^{(tb mod 16) k} (a quarter turn per output register: tb is a multiple of 4).
+// The (P, Q) table is indexed by bin (zero out of band: the reference's zero fill) in lane order.
+// tools/fs_model.py models the frame step by step against the f64 oracle.
+//
+// Layout for MI355X: one 256-thread workgroup (4 wave64) per frame in flight, 4 workgroups per
+// CU (40 836 B of LDS each fill the 160 KB), persistent grid (CUs x 4) fed by the static-prefix
+// + dynamic-suffix frame schedule of ddc_queue.hpp, the next frame's input prefetched into
+// registers under inverse pass 1, all global memory through raw buffer instructions (scalar base
+// + lane offset), nt IQ stores.
+#include <hip/hip_runtime.h>
+
+#include "ddc_frame_common.hpp"
+#include "ddc_queue.hpp"
+#include "ddc_stamps.hpp"
+#include "ddc_fs_perm.h"
+
+namespace sddc {
+namespace {
+
+#ifdef SDDC_STAMPS
+__device__ unsigned g_fs_stamps[2048 * 4 * kStampWords];
+#endif
+
+__device__ __forceinline__ float dpp_partner(float v)
+{
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, true));
+}
+
+// f += conj(zp) q for the bin pair (k, 15 - k), zp = the partner lane's registers: the DPP
+// operand feeds the FMA directly.  s_nop 1: a DPP read of a VGPR needs two wait states after
+// the VALU write of it (the compiler cannot see into the asm).
+__device__ __forceinline__ void split_dpp2(float2 &fa, float2 &fb, float2 za, float2 zb, float4 qa, float4 qb)
+{
+    asm("s_nop 1\n\t"
+        "v_fmac_f32_dpp %0, %4, %8 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %0, %5, %9 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %1, %4, %9 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %1, -%5, %8 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %2, %6, %10 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %2, %7, %11 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %3, %6, %11 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %3, -%7, %10 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf"
+        : "+v"(fa.x), "+v"(fa.y), "+v"(fb.x), "+v"(fb.y)
+        : "v"(za.x), "v"(za.y), "v"(zb.x), "v"(zb.y), "v"(qa.z), "v"(qa.w), "v"(qb.z), "v"(qb.w));
+}
+
+// Zk P (own registers)
+__device__ __forceinline__ float2 zk_p(float2 zk, float4 c)
+{
+    return make_float2(fmaf(zk.x, c.x, -zk.y * c.y), fmaf(zk.x, c.y, zk.y * c.x));
+}
+__device__ __forceinline__ float2 zc_q(float2 f, float2 zc, float4 c)
+{
+    f.x = fmaf(zc.x, c.z, f.x);
+    f.x = fmaf(zc.y, c.w, f.x);
+    f.y = fmaf(zc.x, c.w, f.y);
+    f.y = fmaf(-zc.y, c.z, f.y);
+    return f;
+}
+
+// v (-i)^s, then the sideband flip (imag sign) when LSB: s and LSB are constants after unrolling,
+// so the whole output stage is at most one sign XOR per component
+template <bool LSB>
+__device__ __forceinline__ float2 quarter_flip(float2 v, int s)
+{
+    s &= 3;
+    float2 o = s == 0 ? v : s == 1 ? make_float2(v.y, -v.x) : s == 2 ? make_float2(-v.x, -v.y) : make_float2(-v.y, v.x);
+    if constexpr (LSB) o.y = -o.y;
+    return o;
+}
+
+template <int QT, bool LSB, bool NCO, bool CS16>
+__device__ __forceinline__ void emit_frame_q(void *__restrict__ out, int fbase, int k, int t, const float2 (&u)[16],
+                                             const OutArgs &oa, const NcoArgs &nco)
+{
+    const __amdgpu_buffer_rsrc_t ro = buf_rsrc(static_cast<char *>(out) + (size_t)fbase * out_bytes<CS16>());
+    const int r0 = k == 0 ? 4 : 0;   // wave-uniform
+#pragma unroll
+    for (int r = 0; r < 12; r++) {
+        if (r < r0) continue;
+        float2 v = quarter_flip<LSB>(u[r], QT * r);
+        if constexpr (NCO) v = nco_mix(v, nco, fbase + t + NT * r);
+        store_iq<CS16>(v, ro, (unsigned)t, (unsigned)(NT * r), oa);
+    }
+}
+
+// The queue wave (not wave 0, which also carries the self-mirrored columns' split)
+constexpr int kQWave = 3;
+// F0 -> F1 exchange: element 16 t + r (F0's row t) at 17 t + r, so F0's 16 stores are one base
+// plus an immediate each (no address VALU) and conflict-free; F1's reads of element
+// t + 256 r at t + (t >> 4) + 272 r are base + immediate too, with one 2-way bank conflict per
+// 32-lane group.  The other exchanges use the first 4096 slots with XOR keys.
+constexpr int kFsLds = HALF + HALF / 16;
+
+template <bool RAND, bool LSB, bool NCO, bool CS16>
+__global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
+    const int *__restrict__ in32, void *__restrict__ out, int nframes, const float2 *__restrict__ tw_p1,
+    const float2 *__restrict__ rec_f, const float4 *__restrict__ pqf, const float2 *__restrict__ fsl, int tunebin,
+    OutArgs oa, NcoArgs nco, unsigned *__restrict__ wq, int kstat)
+{
+    __shared__ __attribute__((aligned(16))) float2 lds[kFsLds];
+    // F1 twiddles W_256^{s r} [15][16] (I1 conjugates them: at d = 0 its table is the same) and
+    // the NS = 256 passes' bases W^j, W^{4j} (j < 256: F2 reads them at the lane's column, I2 at
+    // its thread index).  In LDS, not registers or L2: the L2 loads' waits (vmcnt, in issue
+    // order) would also wait for the input prefetch and the stores.
+    __shared__ __attribute__((aligned(16))) float2 twl[15 * 16];
+    __shared__ __attribute__((aligned(16))) float2 wtab[2 * NT];
+    __shared__ int s_next;   // the workgroup's next frame (the queue wave's schedule), -1 when none is left
+    static_assert(sizeof(float2) * (kFsLds + 15 * 16 + 2 * NT) + sizeof(int) <= 163840 / 4,
+                  "four workgroups per CU");
+
+    const int tid = (int)threadIdx.x;
+    const int w = (int)blockIdx.x;
+    constexpr int QLANE = 64 * kQWave;
+    const bool qw = __builtin_amdgcn_readfirstlane(tid >> 6) == kQWave;
+    FrameSchedule<1> fsch;
+    int x[16];
+    {
+        // every wave knows the first frame (it is static unless the batch is small): its input
+        // loads go out at once, ahead of the table copies
+        const int f0s = fs_static_frame(nframes, (int)gridDim.x, w, 0, kstat);
+        if (f0s >= 0) load_frame(in32, f0s / FRAMES, f0s % FRAMES, x);
+        if (qw) {
+            int f0[1];
+            fsch.init(wq, nframes, w, (int)gridDim.x, kstat, f0);
+            if (tid == QLANE) s_next = f0[0];
+        }
+        for (int i = tid; i < 15 * 16; i += NT) twl[i] = tw_p1[i];
+        wtab[tid] = rec_f[tid];
+        wtab[NT + tid] = rec_f[NT + tid];
+        __syncthreads();
+        const int f = s_next;
+        if (f >= 0 && f0s < 0) load_frame(in32, f / FRAMES, f % FRAMES, x);
+    }
+    int f = s_next;
+    int blk = f / FRAMES, k = f - blk * FRAMES;
+    const int col_ = kFsPerm[tid];
+    const int qt = (tunebin >> 2) & 3;   // (tb mod 16) / 4: the output quarter turns
+    const bool w0 = __builtin_amdgcn_readfirstlane(tid >> 6) == 0;   // the wave holding columns 0, 128
+    ST_INIT();
+
+    while (f >= 0) {
+        if (qw) fsch.peek();
+        // opaque per-frame copies of the thread index and column: without them the compiler
+        // hoists every loop-invariant LDS address out of the frame loop and spills them
+        int z = 0;
+        asm volatile("" : "+s"(z));
+        const int t = tid + z;
+        const int c = col_ + z;
+        const int sT = swz(t);
+        const int x15 = t & 15;
+        const unsigned xa1 = 2048u * (unsigned)(t >> 4) + 8u * (unsigned)x15;   // st_row base of the F1 / I1 rows
+        const int oblk = blk * 8 * HALF;
+        const int kc = k;
+        // ---- F0 (R16, NS1): convert + DFT16 from registers ----
+        float2 v[16];
+        {
+            float2 a[16];
+#pragma unroll
+            for (int r = 0; r < 16; r++)
+                if constexpr (RAND) {
+                    // convert_float<rand> (fft_mt_r2iq.h:36-51) on the int16 pair: an odd sample is
+                    // XORed with 0xFFFE, i.e. word ^ (word & 0x10001) * 0xFFFE, integer-exact
+                    const int wd = x[r] ^ (int)(((unsigned)x[r] & 0x10001u) * 0xFFFEu);
+                    a[r] = make_float2((float)(int)(short)(wd & 0xffff), (float)(wd >> 16));
+                } else {
+                    a[r] = make_float2((float)(int)(short)(x[r] & 0xffff), (float)(x[r] >> 16));
+                }
+            dft16<-1>(a, v);
+        }
+        ST_SYNC(0);   // the previous frame's last LDS reads are done
+        {
+            float2 *const row = lds + 17 * t;
+#pragma unroll
+            for (int r = 0; r < 16; r++) row[r] = v[r];
+        }
+        ST_SYNC(1);
+        // ---- F1 (R16, NS16): table twiddles W_256^{(t%16) r} ----
+        {
+            float2 a[16];
+            const float2 *const col = lds + t + (t >> 4);
+#pragma unroll
+            for (int r = 0; r < 16; r++) XRD(a[r], col[272 * r]);
+            table_twiddle<-1, true>(a, twl, 16, x15);
+            dft16<-1>(a, v);
+        }
+        ST_SYNC(2);
+#pragma unroll
+        for (int r = 0; r < 16; r++) st_row(lds, xa1, r, 16, v[r]);   // element 256 (t >> 4) + 16 r + (x15 ^ r)
+        ST_SYNC(3);
+        // ---- F2 (R16, NS256) on column c: Z[c + 256 k] in v[k] ----
+        // The split's (P, Q) loads (bin pairs p, 15 - p) run a pair ahead of their use, the first
+        // issued before F2 so that its reads and arithmetic cover the L2 latency (an empty asm
+        // with a memory clobber pins each group; the compiler's own schedule waits for every pair
+        // right after issuing it).  Two pairs ahead of F2 spill at 128 VGPRs.
+        const __amdgpu_buffer_rsrc_t rpq = buf_rsrc(pqf + z);
+        const unsigned t16 = 16u * (unsigned)t;
+        float4 qa[8], qb[8];
+        qa[0] = buf_load16(rpq, t16, 0);
+        qb[0] = buf_load16(rpq, t16, 16u * NT * 15);
+        asm volatile("" ::: "memory");
+        {
+            float2 a[16];
+            const int sC = swz(c);
+#pragma unroll
+            for (int r = 0; r < 16; r++) XRD(a[r], lds[sC + NT * r]);
+            const float2 fw1 = wtab[c], fw4 = wtab[NT + c];   // W^c, W^{4c}
+            twiddle_rec16<-1>(a, fw1, fw4);
+            dft16<-1>(a, v);
+        }
+        // ---- split x filter (bins c + 256 k, mirror from the partner lane) -> I0 DFT ----
+        float2 u[16];
+        {
+            float2 a[16];
+            if (!w0) {
+#pragma unroll
+                for (int p = 0; p < 8; p++) {
+                    if (p + 1 < 8) {
+                        qa[p + 1] = buf_load16(rpq, t16, 16u * NT * (p + 1));
+                        qb[p + 1] = buf_load16(rpq, t16, 16u * NT * (14 - p));
+                        asm volatile("" ::: "memory");
+                    }
+                    float2 fa = zk_p(v[p], qa[p]), fb = zk_p(v[15 - p], qb[p]);
+                    split_dpp2(fa, fb, v[15 - p], v[p], qa[p], qb[p]);
+                    a[p] = fa;
+                    a[15 - p] = fb;
+                }
+            } else {
+                // wave 0: lanes 0 (column 0: mirror of register k is its own (16 - k) mod 16) and
+                // 1 (column 128: its own 15 - k) are self-mirrored
+                const int lane = t & 63;
+#pragma unroll
+                for (int p = 0; p < 8; p++) {
+                    if (p + 1 < 8) {
+                        qa[p + 1] = buf_load16(rpq, t16, 16u * NT * (p + 1));
+                        qb[p + 1] = buf_load16(rpq, t16, 16u * NT * (14 - p));
+                        asm volatile("" ::: "memory");
+                    }
+#pragma unroll
+                    for (int h = 0; h < 2; h++) {
+                        const int kk = h ? 15 - p : p;
+                        const float4 q = h ? qb[p] : qa[p];
+                        const float2 vm = v[15 - kk], v0m = v[(16 - kk) & 15];
+                        float2 zc = make_float2(dpp_partner(vm.x), dpp_partner(vm.y));
+                        zc = lane == 1 ? vm : zc;
+                        zc = lane == 0 ? v0m : zc;
+                        a[kk] = zc_q(zk_p(v[kk], q), zc, q);
+                    }
+                }
+            }
+            dft16<+1>(a, u);
+        }
+        ST_SYNC(4);   // every wave's F2 reads are done
+        {
+            // row 16 c + (r ^ (swz(c) & 15)): the key XORs in c >> 4 so that the lane pairs c, -c
+            // (equal c mod 16 for c = 0, 8 mod 16) never share a bank (tools/fs_perm.py)
+            const unsigned xc0 = 128u * (unsigned)c + 8u * (unsigned)(swz(c) & 15);
+#pragma unroll
+            for (int r = 0; r < 16; r++) st_row(lds, xc0, r, 0, u[r]);
+        }
+        // the next frame (static, or the ticket read at this frame's top), then a ticket for the
+        // one after it when that one is dynamic (ddc_queue.hpp)
+        if (qw) {
+            const int f_n = fsch.next();
+            if (tid == QLANE) s_next = f_n;
+        }
+        ST_SYNC(5);
+        // I2's lane factors g_t, g_t W^{-t}, g_t W^{-4t} (exactly rounded, from the per-tunebin
+        // table): issued ahead of the input prefetch, so that their wait does not include it
+        const __amdgpu_buffer_rsrc_t rfs = buf_rsrc(fsl);
+        const unsigned t8 = 8u * (unsigned)t;
+        const float2 g0 = buf_load8(rfs, t8, 0), g1 = buf_load8(rfs, t8, 8u * NT), g4 = buf_load8(rfs, t8, 16u * NT);
+        int fn;
+        // ---- I1 (R16, NS16): table twiddles W_256^{-(t%16) r} ----
+        {
+            float2 a[16];
+            // element j + 256 r was stored by I0 column (j >> 4) + 16 r under the key
+            // swz(column) & 15 = (j >> 4) ^ r: byte (8 sT ^ 8 r) + 2048 r, one v_xor per read
+            const unsigned sT8 = 8u * (unsigned)sT;
+#pragma unroll
+            for (int r = 0; r < 16; r++)
+                XRD(a[r], *reinterpret_cast<const float2 *>(reinterpret_cast<const char *>(lds) + ((sT8 ^ (8u * r)) + 2048u * r)));
+            // the next frame's number is read behind the data reads (its LDS round trip under
+            // theirs), and its input loads are issued here rather than in F0, so their 16
+            // registers are free through F2 and the split
+            fn = s_next;
+            if (fn >= 0) {
+                blk = fn / FRAMES;
+                k = fn - blk * FRAMES;
+                load_frame(in32, blk, k, x);
+            }
+            table_twiddle<+1, true>(a, twl, 16, x15);
+            dft16<+1>(a, u);
+        }
+        ST_SYNC(6);
+        {
+            // the same addresses as the F1 stores: recomputed from an opaque copy of t, or the
+            // compiler keeps them live through F2 and spills
+            int t1 = t;
+            asm volatile("" : "+v"(t1));
+            const unsigned xb1 = 2048u * (unsigned)(t1 >> 4) + 8u * (unsigned)(t1 & 15);
+#pragma unroll
+            for (int r = 0; r < 16; r++) st_row(lds, xb1, r, 16, u[r]);
+        }
+        ST_SYNC(7);
+        // ---- I2 (R16, NS256): twiddles g_t W^{-t r}, quarter turns, overlap-discard ----
+        {
+            float2 a[16];
+#pragma unroll
+            for (int r = 0; r < 16; r++) XRD(a[r], lds[sT + NT * r]);
+            const float2 rw1 = wtab[t], rw4 = wtab[NT + t];   // W^t, W^{4t}
+            twiddle_g16<+1>(a, g0, g1, g4, rw1, rw4);
+            dft16<+1>(a, u);
+            const int fb = oblk + emit_base<HALF>(kc);
+            switch (qt) {
+            case 0: emit_frame_q<0, LSB, NCO, CS16>(out, fb, kc, t, u, oa, nco); break;
+            case 1: emit_frame_q<1, LSB, NCO, CS16>(out, fb, kc, t, u, oa, nco); break;
+            case 2: emit_frame_q<2, LSB, NCO, CS16>(out, fb, kc, t, u, oa, nco); break;
+            default: emit_frame_q<3, LSB, NCO, CS16>(out, fb, kc, t, u, oa, nco); break;
+            }
+        }
+        ST_FRAME_END();
+        f = fn;
+    }
+    ST_WRITE(g_fs_stamps, w, tid);
+    if (tid == QLANE) fs_queue_done(wq, (unsigned)gridDim.x);
+}
+
+// FS tables of one tunebin: pqf[l + 256 k] = (P, Q) of bin b = kFsPerm[l] + 256 k (inverse input
+// m = (b - tb) mod 4096, zero unless b is in the reference's band: tb <= b < tb + 2048, b < 4096,
+// or tb - 2048 <= b < tb); fsl = [g_t | g_t W^{-t} | g_t W^{-4t}], g_t = e^{-2 pi i tb t / 4096},
+// looked up exactly in the 4096-point table.
+__global__ void build_fs_tables_kernel(const float2 *__restrict__ hsel0, const float2 *__restrict__ post8192,
+                                       const float2 *__restrict__ tw4096, int tunebin, float4 *__restrict__ pqf,
+                                       float2 *__restrict__ fsl)
+{
+    const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (i >= HALF) return;
+    const int l = i & (NT - 1), kk = i >> 8;
+    const int b = kFsPerm[l] + NT * kk;
+    const bool band = (b >= tunebin && b - tunebin < HALF / 2) || (b < tunebin && tunebin - b <= HALF / 2);
+    float4 c = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (band) {
+        const int m = (b - tunebin) & (HALF - 1);
+        const double hr = hsel0[m].x, hi = hsel0[m].y;
+        const double wr = post8192[b].x, wi = post8192[b].y;
+        const double pr = 1.0 + wi, pi = -wr, qr = 1.0 - wi, qi = wr;   // 1 - i W, 1 + i W
+        c.x = (float)(hr * pr - hi * pi);
+        c.y = (float)(hr * pi + hi * pr);
+        c.z = (float)(hr * qr - hi * qi);
+        c.w = (float)(hr * qi + hi * qr);
+    }
+    pqf[i] = c;
+    if (i < NT) {
+        fsl[i] = tw4096[(tunebin * i) & (HALF - 1)];
+        fsl[NT + i] = tw4096[((tunebin - 1) * i) & (HALF - 1)];
+        fsl[2 * NT + i] = tw4096[((tunebin - 4) * i) & (HALF - 1)];
+    }
+}
+
+template <bool RAND, bool LSB, bool NCO, bool CS16>
+hipError_t launch_fs_v(const KernelTables &t, const int16_t *d_in, int nblk, void *d_out, const float4 *pqf,
+                       const float2 *fsl, int tunebin, const OutArgs &oa, const NcoArgs &nco, unsigned *wq,
+                       int static_pct, int device, hipStream_t s)
+{
+    auto kern = r2iq_fs_kernel<RAND, LSB, NCO, CS16>;
+    int occ = 0, cus = 0;
+    hipError_t e = launch_geometry(t.lc, reinterpret_cast<const void *>(kern), NT, device, &occ, &cus);
+    if (e != hipSuccess) return e;
+    const int nframes = nblk * FRAMES;
+    int grid = cus * occ;
+    if (grid > nframes) grid = nframes;
+    const int kstat = frame_schedule_kstat(nframes, grid, static_pct);
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), 0, s, reinterpret_cast<const int *>(d_in), d_out, nframes,
+                       t.tw_p1, t.rec_f, pqf, fsl, tunebin, oa, nco, wq, kstat);
+    return hipGetLastError();
+}
+
+template <bool RAND, bool LSB>
+hipError_t launch_fs_rl(const KernelTables &t, const int16_t *d_in, int nblk, void *d_out, const float4 *pqf,
+                        const float2 *fsl, int tunebin, bool cs16, const OutArgs &oa, const NcoArgs &nco,
+                        unsigned *wq, int static_pct, int device, hipStream_t s)
+{
+    if (nco.starts)
+        return cs16 ? launch_fs_v<RAND, LSB, true, true>(t, d_in, nblk, d_out, pqf, fsl, tunebin, oa, nco, wq, static_pct, device, s)
+                    : launch_fs_v<RAND, LSB, true, false>(t, d_in, nblk, d_out, pqf, fsl, tunebin, oa, nco, wq, static_pct, device, s);
+    return cs16 ? launch_fs_v<RAND, LSB, false, true>(t, d_in, nblk, d_out, pqf, fsl, tunebin, oa, nco, wq, static_pct, device, s)
+                : launch_fs_v<RAND, LSB, false, false>(t, d_in, nblk, d_out, pqf, fsl, tunebin, oa, nco, wq, static_pct, device, s);
+}
+
+}  // namespace
+
+bool fs_path(int d, int tunebin) { return d == 0 && (tunebin & 3) == 0; }
+
+hipError_t launch_build_fs_tables(const KernelTables &t, int tunebin, float4 *pqf, float2 *fsl, hipStream_t s)
+{
+    if (tunebin < 0 || tunebin >= HALF || (tunebin & 3)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(build_fs_tables_kernel, dim3(HALF / 256), dim3(256), 0, s, t.hsel[0], t.post8192, t.tw4096,
+                       tunebin, pqf, fsl);
+    return hipGetLastError();
+}
+
+hipError_t launch_frames_fs(const KernelTables &t, const int16_t *d_in, int nblk, void *d_out, const float4 *pqf,
+                            const float2 *fsl, int tunebin, int lsb, int rand, int cs16, float cs16_scale,
+                            const float2 *nco_starts, const float2 *nco_trig, unsigned *wq, int static_pct,
+                            int device, hipStream_t s)
+{
+    if (tunebin & 3) return hipErrorInvalidValue;
+    if (static_pct < 0 || static_pct > 100) return hipErrorInvalidValue;
+    const OutArgs oa{0u, cs16_scale};   // the sideband flip is a template parameter here
+    const NcoArgs nco{nco_starts, nco_trig};
+    const bool c = cs16 != 0;
+    if (rand)
+        return lsb ? launch_fs_rl<true, true>(t, d_in, nblk, d_out, pqf, fsl, tunebin, c, oa, nco, wq, static_pct, device, s)
+                   : launch_fs_rl<true, false>(t, d_in, nblk, d_out, pqf, fsl, tunebin, c, oa, nco, wq, static_pct, device, s);
+    return lsb ? launch_fs_rl<false, true>(t, d_in, nblk, d_out, pqf, fsl, tunebin, c, oa, nco, wq, static_pct, device, s)
+               : launch_fs_rl<false, false>(t, d_in, nblk, d_out, pqf, fsl, tunebin, c, oa, nco, wq, static_pct, device, s);
+}
+
+}  // namespace sddc
+
+// Diagnostic (SDDC_STAMPS builds only): copy the d = 0 fused-split kernel's stamp buffer of the
+// last launch ([workgroup][wave][words], tools/fs_stamps.py) to host memory; -1 in product builds.
+extern "C" int sddc_ddc_internal_fs_stamps(unsigned *host, int nwords, int *words_per_wave)
+{
+    if (words_per_wave) *words_per_wave = sddc::kStampWords;
+#ifdef SDDC_STAMPS
+    const size_t n = sizeof(sddc::g_fs_stamps) / sizeof(unsigned);
+    if (!host || nwords < 0 || (size_t)nwords > n) return -2;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(sddc::g_fs_stamps), (size_t)nwords * sizeof(unsigned), 0,
+                               hipMemcpyDeviceToHost) == hipSuccess ? 0 : -3;
+#else
+    (void)host;
+    (void)nwords;
+    return -1;
+#endif
+}

@@ -70,28 +70,32 @@ struct KernelTables {
 // nco_starts/nco_trig: fused fine-tune NCO tables (fine_tune.h), or nullptr for none.
 // cs16: write saturate(rint(x * cs16_scale)) int16 (I, Q) pairs instead of complex float.
 // wq: a zeroed dynamic-frame-queue slot (kFsQueueWords unsigned words), left zeroed.
+// static_pct: the share (percent) of each workgroup's frames taken statically before it draws
+// from the queue (ddc_queue.hpp FrameSchedule); kPStaticPct[d] by default.
 hipError_t launch_frames_persistent(const KernelTables &t, int d, const int16_t *d_in, int nblk,
                                     void *d_out, const float4 *pq, int tunebin, int lsb, int rand,
                                     int cs16, float cs16_scale, const float2 *nco_starts,
-                                    const float2 *nco_trig, unsigned *wq, int device, hipStream_t s);
+                                    const float2 *nco_trig, unsigned *wq, int static_pct, int device,
+                                    hipStream_t s);
+constexpr int kPStaticPct[7] = {75, 75, 75, 75, 75, 75, 75};
 hipError_t launch_build_split_filter(const KernelTables &t, int d, int tunebin, float4 *pq, hipStream_t s);
 
-// d = 0 fused-split kernel (ddc_persistent.hip, FS): used when fs_path(d, tunebin) (d = 0, tunebin a
-// multiple of 4, built with SDDC_D0_FS).  Its per-tunebin tables: pqf (4096 float4, the split x
-// filter by bin in lane order) and fsl (3 x 256 float2, the output modulation's lane factors),
-// built by launch_build_fs_tables.
-#ifndef SDDC_D0_FS
-#define SDDC_D0_FS 1
-#endif
+// d = 0 fused-split kernel (ddc_fs.hip, FS): used when fs_path(d, tunebin) (d = 0, tunebin a
+// multiple of 4: every tune bin setFreqOffset produces, fft_mt_r2iq.cpp:104).  Its per-tunebin
+// tables: pqf (4096 float4, the split x filter by bin in lane order) and fsl (3 x 256 float2, the
+// output modulation's lane factors), built by launch_build_fs_tables.
 bool fs_path(int d, int tunebin);
 hipError_t launch_build_fs_tables(const KernelTables &t, int tunebin, float4 *pqf, float2 *fsl, hipStream_t s);
 // wq: a zeroed slot of kFsQueueWords unsigned words (the dynamic frame queue); the launch leaves it
 // zeroed again.  Launches that may run at the same time need different slots.
+// static_pct: the share (percent) of each workgroup's frames taken statically before it draws
+// from the queue (ddc_queue.hpp FrameSchedule); kFsStaticPct by default.
 constexpr int kFsQueueWords = 16 * 9;
+constexpr int kFsStaticPct = 75;
 hipError_t launch_frames_fs(const KernelTables &t, const int16_t *d_in, int nblk, void *d_out, const float4 *pqf,
                             const float2 *fsl, int tunebin, int lsb, int rand, int cs16, float cs16_scale,
-                            const float2 *nco_starts, const float2 *nco_trig, unsigned *wq, int device,
-                            hipStream_t s);
+                            const float2 *nco_starts, const float2 *nco_trig, unsigned *wq, int static_pct,
+                            int device, hipStream_t s);
 
 // many-channel v2 (d = 4..6): persistent, forward once per (frame, 128-channel chunk)
 // stride: scalar components (float or int16) per channel row; cs16 as above.  d_windows:

@@ -119,6 +119,72 @@ struct FsQueue {
         return dry ? -1 : lo + pv;
     }
 };
+// Static prefix + dynamic suffix: each workgroup first takes kstat static frames of its home
+// shard (fs_static_frame, interleaved: static frame i is lo_s + i nwg_s + blockIdx / 8), with no
+// atomic, and only then draws from the shard's queue (tickets count from past the static frames).
+// The queue absorbs the imbalance (the SIMDs arbitrate by age, so the four workgroups of a CU run
+// at different speeds) and the tail; the static prefix saves its per-frame cost (one device-scope
+// atomic round trip, ~1000 cycles of the queue wave per frame, which the other waves wait for at
+// the next barrier) for most frames.  kstat is chosen on the host (a fraction of the frames per
+// workgroup small enough that the slowest workgroup of a CU still finishes its static frames
+// before the queue runs dry).
+// Worked by the queue wave only (all bookkeeping wave-uniform, scalar).  Per frame j of the
+// workgroup's sequence: at the frame top, top() reads a pending ticket (taken a frame earlier);
+// at inverse pass 0, next() returns frame j + 1 (static, or the pending ticket resolved) and takes
+// the ticket for frame j + 2 when that one is dynamic.
+// LA: lookahead, the number of frames known ahead of the current one (1: the FS kernel, which
+// learns frame j + 1 at frame j's inverse pass 0; 2: the persistent kernel, which prefetches
+// frame j + 1 at frame j's top and learns frame j + 2 in frame j's middle).
+template <int LA>
+struct FrameSchedule {
+    FsQueue q;
+    int j = 0;      // index of the current frame in the workgroup's sequence
+    int kw = 0;     // this workgroup's static frames: slo + i nwg, i < kw
+    int slo, nwg;
+
+    // frame i < LA of the sequence: static, or from the queue at once (small batches)
+    __device__ __forceinline__ int first(int i)
+    {
+        if (i < kw) return slo + i * nwg;
+        q.take();
+        q.peek();
+        return q.resolve();
+    }
+    // sets up the schedule; f[0..LA) receive the first LA frames (-1: none)
+    __device__ __forceinline__ void init(unsigned *wq, int nframes, int w, int grid, int kstat, int (&f)[LA])
+    {
+        const int s = w & (FS_SHARDS - 1);
+        nwg = fs_shard_nwg(grid, s);
+        slo = fs_shard_lo(nframes, s) + w / FS_SHARDS;
+        const int pre = fs_shard_pre(nframes, grid, s, kstat);
+        kw = pre > w / FS_SHARDS ? (pre - w / FS_SHARDS + nwg - 1) / nwg : 0;
+        q.init(wq, nframes, s, grid, kstat);
+        for (int i = 0; i < LA; i++) f[i] = first(i);
+        if (LA >= kw) q.take();   // frame LA is dynamic: its ticket now
+    }
+    // reads the pending ticket, if any (taken a frame earlier): call at a point where its wait
+    // is free, before next()
+    __device__ __forceinline__ void peek()
+    {
+        if (j + LA >= kw) q.peek();
+    }
+    // frame j + LA, and the ticket for frame j + LA + 1 when that one is dynamic; then j++
+    __device__ __forceinline__ int next()
+    {
+        const int fn = j + LA < kw ? slo + (j + LA) * nwg : q.resolve();
+        if (j + LA + 1 >= kw) q.take();
+        j++;
+        return fn;
+    }
+};
+
+// static frames per workgroup for a static share of pct percent (at least one)
+inline int frame_schedule_kstat(int nframes, int grid, int pct)
+{
+    const int k = (int)((long long)nframes * pct / (100LL * grid));
+    return k < 1 ? 1 : k;
+}
+
 __device__ __forceinline__ void fs_queue_done(unsigned *wq, unsigned grid)
 {
     if (atomicAdd(wq + 16 * FS_SHARDS, 1u) == grid - 1) {

@@ -108,6 +108,15 @@ struct Readers {
             }
         return hipSuccess;
     }
+    // stream s waits for the last recorded launch on stream `other` (nothing to do when other is
+    // s, or when `other` has no entry: entries are dropped only after a host sync of all of them)
+    hipError_t order_after(hipStream_t other, hipStream_t s) const
+    {
+        if (other == s) return hipSuccess;
+        for (const auto &p : v)
+            if (p.first == other) return hipStreamWaitEvent(s, p.second, 0);
+        return hipSuccess;
+    }
     // the host waits for every reader (before a synchronous copy or a free)
     hipError_t sync() const
     {
@@ -200,20 +209,35 @@ struct sddc_ddc {
 
     // split x filter coefficients of the current (d, tunebin), rebuilt on device when either
     // changes; readers = the streams of single-channel launches that read them (and d_nco)
+    // Each table set remembers the stream its last rebuild ran on (pq_s, wave_s, fs_s): a launch
+    // on another stream first waits for that stream's last recorded launch (Readers::order_after),
+    // which is behind the rebuild (a rebuild is recorded like a launch).
     float4 *d_pq = nullptr;
     int pq_d = -1, pq_tb = -1;
+    hipStream_t pq_s = nullptr;
     // the d = 0 wave kernel's per-tunebin tables: pqW (4096 float4) then twI (4096 float2)
     float4 *d_wave = nullptr;
     int wave_tb = -1;
+    hipStream_t wave_s = nullptr;
     // the d = 0 fused-split kernel's per-tunebin tables: pqf (4096 float4) then fsl (768 float2)
     float4 *d_fs = nullptr;
     int fs_tb = -1;
-    // the single-channel kernels' dynamic frame queues: a ring of kQueueSlots zeroed slots, one per
-    // launch in turn (each launch leaves its slot zeroed; the ring lets launches on different
-    // streams overlap)
+    hipStream_t fs_s = nullptr;
+    // the single-channel kernels' dynamic frame queues: a ring of kQueueSlots slots, one per launch
+    // in turn.  A slot is zero when its launch starts and its last workgroup zeroes it again, so
+    // the slot's next launch must start after that launch has finished: on the same stream that
+    // is stream order; on another stream it waits for the slot's stream (q_s).  A slot whose
+    // launch failed, or every slot after a HIP error, is zeroed stream-ordered before its next use.
     static constexpr int kQueueSlots = 64;
     unsigned *d_queue = nullptr;
     int queue_slot = 0;
+    int fs_static_pct = sddc::kFsStaticPct;   // the d = 0 kernel's static share of frames (ddc_queue.hpp)
+    int p_static_pct[SDDC_DDC_NDEC] = {sddc::kPStaticPct[0], sddc::kPStaticPct[1], sddc::kPStaticPct[2],
+                                       sddc::kPStaticPct[3], sddc::kPStaticPct[4], sddc::kPStaticPct[5],
+                                       sddc::kPStaticPct[6]};   // the persistent kernel's, per d
+    hipStream_t q_s[kQueueSlots] = {};
+    bool q_used[kQueueSlots] = {};
+    bool q_dirty[kQueueSlots] = {};
     Readers readers;
 
     // fused fine-tune NCO: host chain + per-launch [T | lane starts] staged through a
@@ -393,8 +417,10 @@ int sddc_ddc_create(float gain, int device, sddc_ddc_t **out)
     if (e == hipSuccess) e = hipMalloc(&h->d_fs, 4096 * sizeof(float4) + 768 * sizeof(float2));
     if (e == hipSuccess)
         e = hipMalloc(&h->d_queue, (size_t)sddc_ddc::kQueueSlots * sddc::kFsQueueWords * sizeof(unsigned));
-    if (e == hipSuccess)
-        e = hipMemset(h->d_queue, 0, (size_t)sddc_ddc::kQueueSlots * sddc::kFsQueueWords * sizeof(unsigned));
+    if (e == hipSuccess)   // zeroed on the handle's stream and waited for: the first launch may be on any stream
+        e = hipMemsetAsync(h->d_queue, 0, (size_t)sddc_ddc::kQueueSlots * sddc::kFsQueueWords * sizeof(unsigned),
+                           h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
     if (e != hipSuccess) {
         sddc_ddc_destroy(h);
         return fail(SDDC_ERR_HIP, "create: %s", hipGetErrorString(e));
@@ -592,15 +618,58 @@ static hipError_t stage_nco(sddc_ddc_t *h, int nblk, hipStream_t s)
     return hipEventRecord(h->nco_ev[slot], s);
 }
 
-// the next slot of the handle's dynamic-frame-queue ring (under h->mu, like every launch)
-static unsigned *next_queue_slot(sddc_ddc_t *h)
+// The next slot of the handle's dynamic-frame-queue ring for a launch on s (under h->mu, like
+// every launch): ordered after the slot's previous launch, or zeroed first if that launch failed.
+// *slot receives its index for queue_slot_launched.
+static hipError_t next_queue_slot(sddc_ddc_t *h, hipStream_t s, unsigned **wq, int *slot)
 {
-    unsigned *wq = h->d_queue + (size_t)h->queue_slot * sddc::kFsQueueWords;
-    h->queue_slot = (h->queue_slot + 1) % sddc_ddc::kQueueSlots;
-    return wq;
+    const int i = h->queue_slot;
+    h->queue_slot = (i + 1) % sddc_ddc::kQueueSlots;
+    *slot = i;
+    *wq = h->d_queue + (size_t)i * sddc::kFsQueueWords;
+    hipError_t e = hipSuccess;
+    if (h->q_dirty[i]) {
+        if (h->q_used[i]) e = h->readers.order_after(h->q_s[i], s);   // the failed launch may still run
+        if (e == hipSuccess) e = hipMemsetAsync(*wq, 0, sddc::kFsQueueWords * sizeof(unsigned), s);
+        if (e == hipSuccess) h->q_dirty[i] = false;
+    } else if (h->q_used[i]) {
+        e = h->readers.order_after(h->q_s[i], s);
+    }
+    return e;
 }
 
+// after the launch that took slot i: on success the slot's last user is s (the launch is recorded
+// in readers right after); on failure the slot is zeroed before its next use
+static void queue_slot_launched(sddc_ddc_t *h, int i, hipStream_t s, hipError_t e)
+{
+    h->q_s[i] = s;
+    h->q_used[i] = true;
+    if (e != hipSuccess) h->q_dirty[i] = true;
+}
+
+// a HIP error on a launch path: the state of every in-flight launch is unknown, so every queue
+// slot is zeroed (stream-ordered) before its next use
+static void queue_mark_all_dirty(sddc_ddc_t *h)
+{
+    for (int i = 0; i < sddc_ddc::kQueueSlots; i++) h->q_dirty[i] = true;
+}
+
+// a launch on s reads a table set last rebuilt on `built`: wait for that rebuild
+static hipError_t order_after_build(sddc_ddc_t *h, hipStream_t built, hipStream_t s)
+{
+    return h->readers.order_after(built, s);
+}
+
+static hipError_t launch_single_impl(sddc_ddc_t *h, const int16_t *d_in, int nblk, void *d_out, hipStream_t s);
+
 static hipError_t launch_single(sddc_ddc_t *h, const int16_t *d_in, int nblk, void *d_out, hipStream_t s)
+{
+    const hipError_t e = launch_single_impl(h, d_in, nblk, d_out, s);
+    if (e != hipSuccess) queue_mark_all_dirty(h);
+    return e;
+}
+
+static hipError_t launch_single_impl(sddc_ddc_t *h, const int16_t *d_in, int nblk, void *d_out, hipStream_t s)
 {
     const sddc_variants_api *V = h->variant ? variants() : nullptr;   // set_variant checked it loads
     if (h->variant == 1) {
@@ -621,9 +690,14 @@ static hipError_t launch_single(sddc_ddc_t *h, const int16_t *d_in, int nblk, vo
         if (h->wave_tb != h->tunebin) {
             hipError_t e = h->readers.order_before(s);   // launches on other streams may still read them
             if (e != hipSuccess) return e;
+            h->wave_tb = -1;
             e = V->build_wave_tables(h->tables, h->tunebin, pqW, twI, s);
+            if (e == hipSuccess) e = h->readers.record(s);
             if (e != hipSuccess) return e;
             h->wave_tb = h->tunebin;
+            h->wave_s = s;
+        } else if (hipError_t e = order_after_build(h, h->wave_s, s); e != hipSuccess) {
+            return e;
         }
         hipError_t e = V->frames_wave(
             h->tables, d_in, nblk, d_out, pqW, twI, h->tunebin, h->lsb, h->rand, h->out_fmt == SDDC_DDC_FMT_CS16,
@@ -639,24 +713,45 @@ static hipError_t launch_single(sddc_ddc_t *h, const int16_t *d_in, int nblk, vo
         if (h->fs_tb != h->tunebin) {
             hipError_t e = h->readers.order_before(s);   // launches on other streams may still read them
             if (e != hipSuccess) return e;
+            h->fs_tb = -1;   // a failed rebuild leaves the tables unknown
             e = sddc::launch_build_fs_tables(h->tables, h->tunebin, pqf, fsl, s);
+            if (e == hipSuccess) e = h->readers.record(s);
             if (e != hipSuccess) return e;
             h->fs_tb = h->tunebin;
+            h->fs_s = s;
+        } else if (hipError_t e = order_after_build(h, h->fs_s, s); e != hipSuccess) {
+            return e;
         }
-        unsigned *wq = next_queue_slot(h);
-        hipError_t e = sddc::launch_frames_fs(h->tables, d_in, nblk, d_out, pqf, fsl, h->tunebin, h->lsb, h->rand,
-                                              h->out_fmt == SDDC_DDC_FMT_CS16, h->cs16_scale, nco_starts, nco_trig,
-                                              wq, h->device, s);
+        unsigned *wq = nullptr;
+        int qi = 0;
+        hipError_t e = next_queue_slot(h, s, &wq, &qi);
+        if (e != hipSuccess) return e;
+        e = sddc::launch_frames_fs(h->tables, d_in, nblk, d_out, pqf, fsl, h->tunebin, h->lsb, h->rand,
+                                   h->out_fmt == SDDC_DDC_FMT_CS16, h->cs16_scale, nco_starts, nco_trig, wq,
+                                   h->fs_static_pct, h->device, s);
+        queue_slot_launched(h, qi, s, e);
         if (e != hipSuccess) return e;
         return h->readers.record(s);
     }
     if (h->pq_d != h->d || h->pq_tb != h->tunebin) {
         hipError_t e = h->readers.order_before(s);   // launches on other streams may still read d_pq
         if (e != hipSuccess) return e;
+        h->pq_d = h->pq_tb = -1;
         e = sddc::launch_build_split_filter(h->tables, h->d, h->tunebin, h->d_pq, s);
+        if (e == hipSuccess) e = h->readers.record(s);
         if (e != hipSuccess) return e;
         h->pq_d = h->d;
         h->pq_tb = h->tunebin;
+        h->pq_s = s;
+    } else if (hipError_t e = order_after_build(h, h->pq_s, s); e != hipSuccess) {
+        return e;
+    }
+    const bool persistent = !(h->d == 0 && h->variant >= 4 && h->variant <= 7);
+    unsigned *wq = nullptr;
+    int qi = -1;
+    if (persistent) {
+        hipError_t e = next_queue_slot(h, s, &wq, &qi);
+        if (e != hipSuccess) return e;
     }
     hipError_t e = h->d == 0 && h->variant == 7
         ? V->frames_inplace(h->tables, d_in, nblk, d_out, h->d_pq, h->tunebin, h->lsb, h->rand,
@@ -673,7 +768,8 @@ static hipError_t launch_single(sddc_ddc_t *h, const int16_t *d_in, int nblk, vo
                                         h->device, s)
         : sddc::launch_frames_persistent(h->tables, h->d, d_in, nblk, d_out, h->d_pq, h->tunebin, h->lsb, h->rand,
                                          h->out_fmt == SDDC_DDC_FMT_CS16, h->cs16_scale, nco_starts, nco_trig,
-                                         next_queue_slot(h), h->device, s);
+                                         wq, h->p_static_pct[h->d], h->device, s);
+    if (qi >= 0) queue_slot_launched(h, qi, s, e);
     if (e != hipSuccess) return e;
     return h->readers.record(s);
 }
@@ -713,6 +809,25 @@ int sddc_ddc_internal_set_variant(sddc_ddc_t *h, int variant)
     std::lock_guard<std::mutex> lk(h->mu);
     h->variant = variant;
     return SDDC_OK;
+}
+
+/* internal (sddc_ddc_internal.h): a tuning parameter of the kernels, for A/B timing */
+int sddc_ddc_internal_set_param(sddc_ddc_t *h, int param, int value)
+{
+    if (!h) return fail(SDDC_ERR_ARG, "null handle");
+    std::lock_guard<std::mutex> lk(h->mu);
+    switch (param) {
+    case SDDC_DDC_PARAM_FS_STATIC_PCT:
+        if (value < 0 || value > 100) return fail(SDDC_ERR_ARG, "static share %d outside 0..100", value);
+        h->fs_static_pct = value;
+        return SDDC_OK;
+    case SDDC_DDC_PARAM_P_STATIC_PCT:
+        if (value < 0 || value > 100) return fail(SDDC_ERR_ARG, "static share %d outside 0..100", value);
+        for (int &v : h->p_static_pct) v = value;
+        return SDDC_OK;
+    default:
+        return fail(SDDC_ERR_ARG, "unknown parameter %d", param);
+    }
 }
 
 static int check_process_args(sddc_ddc_t *h, const int16_t *in, int nblk, const void *out)

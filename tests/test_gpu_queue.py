@@ -1,0 +1,222 @@
+"""The dynamic frame queue's path against the oracle at headline size (pytest -m gpu).
+
+The single-channel kernels hand frames out from a device-scope queue (ddc_queue.hpp) once a
+launch has more frames than resident workgroups: frames = 11 * nblk against CUs x 4 = 1024
+workgroups.  The small-batch parity tests (test_gpu_parity.py, 1-5 blocks) give every workgroup
+one static frame, so they never take a ticket, hop a shard or run the d = 1, 2 two-static-frame
+start.  Here the launches are 256 and 2048 blocks (the BASELINE C2 batch) into NaN-filled
+outputs, and the HIP output is compared with the f64 oracle (fft_mt_r2iq_impl.hpp:84-138):
+  - every block of the 256-block launches and of the 2048-block d = 0 launch (the headline);
+  - at 2048 blocks for d = 1, 2, 4: 2-block windows at the first, middle and last frame of each
+    of the queue's 8 shards, the last block and random blocks, each window fed its real
+    4096-sample history from the stream.
+Plus the queue ring's reuse across streams (more than kQueueSlots = 64 launches over three
+streams, one of them backed up) and a table rebuild on one stream read by a launch on another.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-5
+BLOCK = 65536
+HIST = 4096
+FRAMES = 11
+
+
+@pytest.fixture(scope="module")
+def torch_dev():
+    import torch
+    assert torch.cuda.is_available(), "gpu tests need a GPU"
+    return torch
+
+
+@pytest.fixture(scope="module")
+def ddc(torch_dev):
+    from extio_sddc_amd import R2iq
+    r = R2iq(gain=1.0, device=0)
+    yield r
+    r.close()
+
+
+@pytest.fixture(scope="module")
+def H(oracle):
+    return oracle.filter_bank(1.0)
+
+
+def device_stream(torch, nblk, seed):
+    """[4096 zero history | nblk blocks] int16 on the GPU: two tones (one strong) + Gaussian noise,
+    the synth 'mix' recipe evaluated on the device (phases in float64)."""
+    n = nblk * BLOCK
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    t = torch.arange(n, dtype=torch.float64, device="cuda")
+    x = 9000 * torch.sin(2 * np.pi * torch.frac(0.0713 * t)) + 3000 * torch.sin(2 * np.pi * torch.frac(0.191 * t))
+    x += 300 * torch.randn(n, dtype=torch.float64, device="cuda", generator=g)
+    del t
+    x = torch.clamp(torch.round(x), -32768, 32767).to(torch.int16)
+    return torch.cat([torch.zeros(HIST, dtype=torch.int16, device="cuda"), x])
+
+
+def run(torch, ddc, d_in, nblk, d, tb, stream=None):
+    from extio_sddc_amd import output_samples
+    ddc.setDecimate(d)
+    ddc.setTuneBin(tb)
+    ddc.setSideband(False)
+    ddc.updateRand(False)
+    d_out = torch.full((output_samples(d, nblk) * 2,), float("nan"), dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    ddc.process_device(d_in, nblk, d_out, stream=stream)
+    torch.cuda.synchronize()
+    return d_out
+
+
+def shard_windows(nblk, extra_seed):
+    """Start blocks of 2-block windows: each of the 8 queue shards' first, middle and last frame
+    (ddc_queue.hpp fs_shard_lo), the last block, and four random blocks."""
+    nframes = FRAMES * nblk
+    starts = set()
+    for s in range(8):
+        lo, hi = (nframes * s) >> 3, (nframes * (s + 1)) >> 3
+        for f in (lo, (lo + hi) // 2, hi - 1):
+            starts.add(min(max(f // FRAMES, 0), nblk - 2))
+    starts.add(nblk - 2)
+    rng = np.random.default_rng(extra_seed)
+    starts.update(int(b) for b in rng.integers(0, nblk - 1, 4))
+    return sorted(starts)
+
+
+def check_windows(oracle, H, x, y, nblk, d, tb, starts):
+    per = 32768 >> d
+    worst = 0.0
+    for b in starts:
+        seg = x[BLOCK * b: HIST + BLOCK * (b + 2)]   # the window's real history + 2 blocks
+        r = oracle.r2iq(seg, 2, d, tb, H=H)
+        yw = y[b * per:(b + 2) * per]
+        err = oracle.max_rel_err(yw, r)
+        worst = max(worst, err)
+        assert err <= TOL, f"d={d} window at block {b}: max-rel-err {err:.3e}"
+    return worst
+
+
+@pytest.mark.parametrize("d", [0, 1, 2, 4])
+def test_queue_path_every_block_256(torch_dev, ddc, oracle, H, d):
+    """256 blocks = 2816 frames: every workgroup takes tickets.  Every output sample vs oracle."""
+    torch = torch_dev
+    nblk, tb = 256, 1024
+    d_in = device_stream(torch, nblk, 0x5DDC + d)
+    y = run(torch, ddc, d_in, nblk, d, tb).cpu().numpy().view(np.complex64)
+    assert np.all(np.isfinite(y)), f"{np.count_nonzero(~np.isfinite(y))} samples never written"
+    x = d_in.cpu().numpy()
+    r = oracle.r2iq(x, nblk, d, tb, H=H)
+    err = oracle.max_rel_err(y, r)
+    assert err <= TOL, f"max-rel-err {err:.3e}"
+
+
+def test_queue_path_headline_every_block(torch_dev, ddc, oracle, H):
+    """The headline launch itself (C2: d = 0, tb 1024, 2048 blocks, 22528 frames in one
+    launch): every frame written, every output sample within 1e-5 of the f64 oracle."""
+    torch = torch_dev
+    nblk, d, tb = 2048, 0, 1024
+    d_in = device_stream(torch, nblk, 0x5DDC)
+    d_out = run(torch, ddc, d_in, nblk, d, tb)
+    assert bool(torch.isfinite(d_out).all()), "frames left unwritten"
+    y = d_out.cpu().numpy().view(np.complex64)
+    del d_out
+    x = d_in.cpu().numpy()
+    del d_in
+    # the oracle in 256-block pieces, each with its real history (bounded host memory)
+    step = 256
+    per = 32768 >> d
+    num = den = 0.0
+    for b0 in range(0, nblk, step):
+        r = oracle.r2iq(x[BLOCK * b0: HIST + BLOCK * (b0 + step)], step, d, tb, H=H)
+        yw = y[b0 * per:(b0 + step) * per]
+        num = max(num, float(np.max(np.abs(yw - r))))
+        den = max(den, float(np.max(np.abs(r))))
+    assert num / den <= TOL, f"max-rel-err {num / den:.3e}"
+
+
+@pytest.mark.parametrize("d", [1, 2, 4])
+def test_queue_path_shard_windows_2048(torch_dev, ddc, oracle, H, d):
+    """2048 blocks at d = 1, 2 (queue with two static frames per workgroup) and d = 4 (static
+    contiguous split): 2-block windows from every shard, the last block and random blocks."""
+    torch = torch_dev
+    nblk, tb = 2048, 1024
+    d_in = device_stream(torch, nblk, 0x5DDC + 16 * d)
+    d_out = run(torch, ddc, d_in, nblk, d, tb)
+    assert bool(torch.isfinite(d_out).all()), "frames left unwritten"
+    y = d_out.cpu().numpy().view(np.complex64)
+    x = d_in.cpu().numpy()
+    check_windows(oracle, H, x, y, nblk, d, tb, shard_windows(nblk, d))
+
+
+@pytest.mark.parametrize("d", [0, 1])
+def test_queue_ring_reuse_across_streams(torch_dev, ddc, d):
+    """More launches than queue slots (72 > 64), round-robin over three streams, the first one
+    backed up behind a 2048-block launch, each into its own NaN-filled output: every output
+    equals the same launch run alone on one stream, bit for bit (no frame dropped or doubled)."""
+    torch = torch_dev
+    from extio_sddc_amd import output_samples
+    nblk, nlaunch, noff = 48, 72, 8
+    d_in = device_stream(torch, 2048, 0x5DDC + 100 + d)
+    ddc.setDecimate(d)
+    ddc.setTuneBin(1024)
+    ddc.setSideband(False)
+    ddc.updateRand(False)
+    n = output_samples(d, nblk) * 2
+    refs = []
+    for o in range(noff):
+        out = torch.full((n,), float("nan"), dtype=torch.float32, device="cuda")
+        ddc.process_device(d_in[o * 3 * BLOCK:], nblk, out)
+        refs.append(out)
+    big = torch.empty(output_samples(d, 2048) * 2, dtype=torch.float32, device="cuda")
+    outs = [torch.full((n,), float("nan"), dtype=torch.float32, device="cuda") for _ in range(nlaunch)]
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    ddc.process_device(d_in, 2048, big, stream=streams[0])   # stream 0 backs up
+    for i in range(nlaunch):
+        o = i % noff
+        ddc.process_device(d_in[o * 3 * BLOCK:], nblk, outs[i], stream=streams[i % 3])
+    torch.cuda.synchronize()
+    for i in range(nlaunch):
+        assert bool(torch.isfinite(outs[i]).all()), f"launch {i}: frames left unwritten"
+        assert torch.equal(outs[i], refs[i % noff]), f"launch {i} differs from the single-stream run"
+    # and the handle still works on its default stream afterwards
+    again = torch.full((n,), float("nan"), dtype=torch.float32, device="cuda")
+    ddc.process_device(d_in, nblk, again)
+    torch.cuda.synchronize()
+    assert torch.equal(again, refs[0])
+
+
+@pytest.mark.parametrize("d,tb0,tb1", [(0, 1024, 2048), (1, 1024, 2048)])
+def test_table_rebuild_seen_by_other_stream(torch_dev, ddc, oracle, H, d, tb0, tb1):
+    """The per-tunebin tables are rebuilt on stream A behind a long launch; a launch on stream B
+    with the same tune bin (no rebuild of its own) must wait for that rebuild, not read the old
+    tables (ddc_runtime.cpp order_after_build)."""
+    torch = torch_dev
+    from extio_sddc_amd import output_samples
+    nblk = 4
+    d_in = device_stream(torch, 2048, 0x5DDC + 200 + d)
+    a, b = torch.cuda.Stream(), torch.cuda.Stream()
+    ddc.setDecimate(d)
+    ddc.setSideband(False)
+    ddc.updateRand(False)
+    ddc.setTuneBin(tb0)
+    n = output_samples(d, nblk) * 2
+    big = torch.empty(output_samples(d, 2048) * 2, dtype=torch.float32, device="cuda")
+    ya = torch.full((n,), float("nan"), dtype=torch.float32, device="cuda")
+    yb = torch.full((n,), float("nan"), dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    ddc.process_device(d_in, 2048, big, stream=a)        # A busy, tables of tb0
+    ddc.setTuneBin(tb1)
+    ddc.process_device(d_in, nblk, ya, stream=a)         # rebuild for tb1, queued on A behind the long launch
+    ddc.process_device(d_in, nblk, yb, stream=b)         # same tb1: no rebuild; must see A's
+    torch.cuda.synchronize()
+    x = d_in[:HIST + nblk * BLOCK].cpu().numpy()
+    r = oracle.r2iq(x, nblk, d, tb1, H=H)
+    for y in (ya, yb):
+        yy = y.cpu().numpy().view(np.complex64)
+        assert oracle.max_rel_err(yy, r) <= TOL
+    assert torch.equal(ya, yb)

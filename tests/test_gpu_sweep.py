@@ -5,8 +5,10 @@ At d = 0 the A/B variants of libsddc_ddc_variants.so (the wave kernel, variant 3
 flight, variant 4; radix 8, variant 5; lane pairs, variant 6; in-place passes, variant 7) are checked on the same case as well.
 
 Bar: IQ max-rel-err <= 1e-5 (north_star) for every channel whose output reaches -40 dB of
-full scale; a channel below that is "leakage-only" and its error is measured against the -40 dB
-level instead (``leak_aware_err``).
+full scale; a channel below that is "leakage-only": its strict error is held to the float32
+floor (<= 2x the oracle's float32 port of the reference algorithm on the same input; the
+distribution over 24 such draws is in test_gpu_floor.py), and, as the documented secondary, its
+error measured against the -40 dB level (``leak_aware_err``) to 1e-5.
 
 Full scale S = 1024 * max|x|: the peak IQ an in-band tone of the input's peak amplitude gives at
 gain 1 (SURVEY.md §8(a) output contract: |IQ| ~ A * 4096 * (2048/8192) * sum(taps)).  A
@@ -16,8 +18,7 @@ criterion is max|y - r| <= 1e-5 * max(max|r|, 10^(-40/20) * S), i.e. the error s
 below the strong tone.  Numbers (seeded draws, the oracle's float32 port as a stand-in for any
 float32 FFT path, the reference's FFTW included): the three leakage-only draws sit at -48.0,
 -56.6 and -58.7 dB with strict errors 1.41e-5, 9.9e-6 and 1.73e-5 and leakage-aware errors
-5.6e-6, 1.5e-6 and 2.0e-6; every other draw is at >= -36 dB and held to the strict bar.
-No bar is derived from the builder's own port any more."""
+5.6e-6, 1.5e-6 and 2.0e-6; every other draw is at >= -36 dB and held to the strict bar."""
 from __future__ import annotations
 
 import ctypes
@@ -78,8 +79,13 @@ def H(oracle):
     return oracle.filter_bank(1.0)
 
 
+@pytest.fixture(scope="module")
+def H32(oracle):
+    return oracle.filter_bank(1.0, np.float32)
+
+
 @pytest.mark.parametrize("d,tb,lsb,rand,src,nblk,seed", _cases())
-def test_random_config_parity(ddc, oracle, H, d, tb, lsb, rand, src, nblk, seed):
+def test_random_config_parity(ddc, oracle, H, H32, d, tb, lsb, rand, src, nblk, seed):
     import torch
     from extio_sddc_amd import _lib, output_samples
     x = make_stream(nblk, src, seed=seed)
@@ -100,12 +106,19 @@ def test_random_config_parity(ddc, oracle, H, d, tb, lsb, rand, src, nblk, seed)
         y = out.cpu().numpy().view(np.complex64)
         assert np.all(np.isfinite(y))
         err, leak = leak_aware_err(y, r, x)
-        if leak:   # the strict error of a leakage-only draw, recorded (the float32 floor)
+        if leak:
+            # primary: at the float32 floor, i.e. within 2x of the oracle's float32 port of the
+            # reference algorithm on the same input (test_gpu_floor.py holds the distribution of
+            # the ratio over 24 such draws to a geometric mean <= 1); the -40 dB rule stays as the
+            # documented secondary
+            port = oracle.r2iq(x, nblk, d, tb, lsb, rand, dtype=np.float32, H=H32)
+            strict, port_err = oracle.max_rel_err(y, r), oracle.max_rel_err(port, r)
             _record({"test": "sweep leakage-only draw", "d": d, "tunebin": tb, "lsb": lsb, "rand": rand,
                      "source": src, "nblk": nblk, "seed": seed, "variant": variant,
                      "peak_db_re_full_scale": 20 * np.log10(float(np.max(np.abs(r))) / (1024.0 * float(
                          np.abs(x.astype(np.float64)).max()))),
-                     "strict_max_rel_err": oracle.max_rel_err(y, r), "leakage_aware_err": err})
+                     "strict_max_rel_err": strict, "port_f32_max_rel_err": port_err, "leakage_aware_err": err})
+            assert strict <= 2.0 * port_err, f"variant {variant}: leakage-only draw {strict:.3e} > 2 x port {port_err:.3e}"
         assert err <= TOL, f"variant {variant}: {'leakage-aware' if leak else 'max-rel'} err {err:.3e}"
 
 

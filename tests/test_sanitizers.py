@@ -80,8 +80,19 @@ def test_handles_from_threads_tsan_cpu(harnesses):
     _run_handles(-1, 4, 3)
 
 
+SAN_STATUS = os.path.join(ROOT, "build", "sanitize_status.txt")
+
+
 @pytest.mark.gpu
 def test_handles_from_threads_tsan_gpu():
-    # prebuilt in the build container (build() / make sanitize): a GPU box runs, never builds
-    assert os.path.exists(HANDLES), "build/tsan/handles_harness missing: make -C extio_sddc_amd/csrc sanitize"
+    # prebuilt in the build container (build() / make sanitize): a GPU box runs, never builds.
+    # A build host without the sanitizer runtimes records why in build/sanitize_status.txt
+    # (__graft_entry__.build); then this is a skip with that reason, not a GPU failure.
+    if not os.path.exists(HANDLES):
+        if os.path.exists(SAN_STATUS):
+            with open(SAN_STATUS) as f:
+                status = f.read().strip()
+            if not status.startswith("ok"):
+                pytest.skip(f"sanitizer harnesses not built on the build host: {status[-300:]}")
+        pytest.fail("build/tsan/handles_harness missing: make -C extio_sddc_amd/csrc sanitize")
     _run_handles(0, 4, 3)

@@ -37,7 +37,9 @@ def main():
     from extio_sddc_amd._lib import SIGNATURES
     dev = torch.device("cuda", 0)
     libs, handles = [], []
-    for p in args.libs:
+    for spec in args.libs:
+        # LIB.so or LIB.so:PARAM=VALUE[,PARAM=VALUE] (sddc_ddc_internal_set_param on its handle)
+        p, _, params = spec.partition(":")
         L = ctypes.CDLL(os.path.abspath(p))
         for name, (res, a) in SIGNATURES.items():
             fn = getattr(L, name)
@@ -53,6 +55,10 @@ def main():
         if args.variant:
             L.sddc_ddc_internal_set_variant.argtypes = [ctypes.c_void_p, ctypes.c_int]
             assert L.sddc_ddc_internal_set_variant(h, args.variant) == 0
+        for kv in filter(None, params.split(",")):
+            k, v = (int(x) for x in kv.split("="))
+            L.sddc_ddc_internal_set_param.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+            assert L.sddc_ddc_internal_set_param(h, k, v) == 0
         libs.append(L)
         handles.append(h)
     nblk = args.nblk
@@ -111,7 +117,7 @@ def main():
             diff = ((outs[i] - outs[0]).abs().max() / outs[0].abs().max()).item()
             gs = nblk * 65536 / (med * 1e-3) / 1e9
             frac = nblk * 65536 * (2 + 4 * nch / (1 << d)) / (med * 1e-3) / 8e12
-            res[f"d{d}:{os.path.basename(p)}"] = {"median_ms": med, "min_ms": ts[0], "GSps": gs, "hbm_frac": frac,
+            res[f"d{d}:{os.path.basename(p)}#{i}"] = {"median_ms": med, "min_ms": ts[0], "GSps": gs, "hbm_frac": frac,
                                                   "maxrel_vs_first": diff, "unwritten_floats": unwritten[i]}
             print(f"d={d} {os.path.basename(p):28s} median {med:.3f} ms min {ts[0]:.3f}  {gs:7.1f} GS/s  "
                   f"roofline {frac*100:5.1f}%  maxrel vs first {diff:.2e}"

@@ -1,9 +1,11 @@
 #!/usr/bin/env python3
-"""Per-segment cycle attribution of the d = 0 fused-split kernel from the SDDC_STAMPS diagnostic
-builds (ddc_persistent.hip: s_memtime right before and after each s_barrier, summed per wave
-over its workgroup's frames; build 1 stamps barriers 0..3, build 2 barriers 4..7).
+"""Per-segment cycle attribution of the single-channel kernels from the SDDC_STAMPS diagnostic
+builds (ddc_stamps.hpp: s_memtime right before and after each s_barrier, summed per wave over its
+workgroup's frames; build 1 stamps barriers 0..3, build 2 barriers 4..7, build 3 barriers 8..11).
 
-  python tools/fs_stamps.py --libs build/ab/stamps1.so build/ab/stamps2.so [--nblk 2048]
+  tools/build_rev_lib.sh tree stamps1   (with EXTRA=-DSDDC_STAMPS=1), likewise stamps2, stamps3
+  python tools/fs_stamps.py --kernel fs --libs build/ab/stamps1.so build/ab/stamps2.so
+  python tools/fs_stamps.py --kernel p --d 4 --libs build/ab/stamps1.so build/ab/stamps2.so
 
 After >= 2 s of back-to-back launches (MI355X_MICROARCH.md "DVFS give-back" item 6) it runs 20
 launches and reads the last one's stamps: per wave index (0..3), the mean over workgroups of
@@ -24,29 +26,48 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-SEGS = 9
+SEGS = 13   # ddc_stamps.hpp kStampSegs
 # barrier i closes the work segment in front of it: what each barrier follows
-WORK = ["F0 convert+DFT (frame start)", "F0 row stores", "F1 reads+twiddle+DFT", "F1 row stores",
-        "F2 reads+DFT, split, I0 DFT", "I0 row stores", "I1 reads+twiddle+DFT", "I1 row stores",
-        "I2 reads+twiddle+DFT+emit"]
+FS_WORK = ["F0 convert+DFT (frame start)", "F0 row stores", "F1 reads+twiddle+DFT", "F1 row stores",
+           "F2 reads+DFT, split, I0 DFT", "I0 row stores (+ queue)", "I1 reads+twiddle+DFT (+ prefetch)",
+           "I1 row stores", "-", "-", "-", "-", "I2 reads+twiddle+DFT+emit (frame end)"]
+P_WORK = {
+    # d = 3 (N = 512): split to LDS, three radix-8 passes on wave 0
+    3: ["F0 convert+DFT (+ prefetch)", "F0 row stores", "F1 reads+twiddle+DFT", "F1 row stores",
+        "F2 reads+twiddle+DFT", "Z stores (+ queue)", "split x filter (Z reads, P/Q loads)", "filtered bins to LDS",
+        "-", "-", "-", "-", "wave-0 inverse tail + emit (frame end)"],
+    # d >= 4 (N <= 256): one filtered bin per thread to sb, wave-0 Stockham tail
+    4: ["F0 convert+DFT (+ prefetch)", "F0 row stores", "F1 reads+twiddle+DFT", "F1 row stores",
+        "F2 reads+twiddle+DFT", "Z stores (+ queue)", "split x filter to sb", "-", "-", "-", "-", "-",
+        "wave-0 inverse tail + emit (frame end)"],
+    # d = 2 (N = 1024): radix-4 pass 0 from registers, 4 workgroup radix-4 passes (3 barriers inside)
+    2: ["F0 convert+DFT (+ prefetch)", "F0 row stores", "F1 reads+twiddle+DFT", "F1 row stores",
+        "F2 reads+twiddle+DFT", "Z stores (+ queue)", "split + I0 DFT-4", "I0 stores", "-", "-", "-", "-",
+        "wg passes + emit (frame end)"],
+    # d = 0, 1 (N = 4096, 2048): radix-N/256, 16, 16 passes
+    1: ["F0 convert+DFT (+ prefetch)", "F0 row stores", "F1 reads+twiddle+DFT", "F1 row stores",
+        "F2 reads+twiddle+DFT", "Z stores (+ queue)", "split + I0 DFT", "I0 row stores", "I1 reads+twiddle+DFT",
+        "I1 row stores", "-", "-", "I2 reads+twiddle+DFT+emit (frame end)"],
+}
 
 
-def run(lib: str, nblk: int, tb: int):
+def run(lib: str, kernel: str, d: int, nblk: int, tb: int):
     import torch
     from extio_sddc_amd._lib import SIGNATURES
     L = ctypes.CDLL(os.path.abspath(lib))
     for name, (res, a) in SIGNATURES.items():
         fn = getattr(L, name)
         fn.restype, fn.argtypes = res, a
-    L.sddc_ddc_internal_fs_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
+    getst = L.sddc_ddc_internal_fs_stamps if kernel == "fs" else L.sddc_ddc_internal_p_stamps
+    getst.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
     h = ctypes.c_void_p()
     assert L.sddc_ddc_create(1.0, 0, ctypes.byref(h)) == 0
     L.sddc_ddc_set_tunebin(h, tb)
-    L.sddc_ddc_set_decimation(h, 0)
+    L.sddc_ddc_set_decimation(h, d)
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(0x5DDC)
     d_in = torch.randint(-32768, 32767, (4096 + nblk * 65536,), dtype=torch.int16, device=dev, generator=g)
-    out = torch.empty(nblk * 32768 * 2, dtype=torch.float32, device=dev)
+    out = torch.empty(nblk * (32768 >> d) * 2, dtype=torch.float32, device=dev)
     s = torch.cuda.current_stream().cuda_stream
     t_end = time.time() + 2.0
     while time.time() < t_end:
@@ -61,10 +82,10 @@ def run(lib: str, nblk: int, tb: int):
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / 20
     wpw = ctypes.c_int()
-    L.sddc_ddc_internal_fs_stamps(None, 0, ctypes.byref(wpw))
+    getst(None, 0, ctypes.byref(wpw))
     ngrid = 256 * 4
     buf = np.zeros(ngrid * 4 * wpw.value, np.uint32)
-    rc = L.sddc_ddc_internal_fs_stamps(buf.ctypes.data, buf.size, None)
+    rc = getst(buf.ctypes.data, buf.size, None)
     assert rc == 0, rc
     L.sddc_ddc_destroy(h)
     return ms, buf.reshape(ngrid, 4, wpw.value)
@@ -73,69 +94,50 @@ def run(lib: str, nblk: int, tb: int):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--libs", nargs="+", required=True)
+    ap.add_argument("--kernel", choices=["fs", "p"], default="fs")
+    ap.add_argument("--d", type=int, default=0)
     ap.add_argument("--nblk", type=int, default=2048)
     ap.add_argument("--tunebin", type=int, default=1024)
     args = ap.parse_args()
+    work = FS_WORK if args.kernel == "fs" else P_WORK[min(args.d, 4) if args.d >= 2 else 1]
     res = {}
     for lib in args.libs:
-        ms, st = run(lib, args.nblk, args.tunebin)
+        ms, st = run(lib, args.kernel, args.d, args.nblk, args.tunebin)
         which = int(st[0, 0, 2 * SEGS + 3])
         fr = st[:, :, 2 * SEGS].astype(np.float64)
         ok = fr > 0
         ticks = st[:, :, 2 * SEGS + 1].astype(np.float64)
         rt = st[:, :, 2 * SEGS + 2].astype(np.float64)
         clk = np.median(ticks[ok] / (rt[ok] * 1e-8)) / 1e9
-        print(f"\n{os.path.basename(lib)} (stamps build {which}): {ms:.4f} ms/launch, in-kernel clock {clk:.3f} GHz, "
-              f"{np.median(ticks[ok] / fr[ok]):.0f} cycles per frame per wave (median)")
+        print(f"\n{os.path.basename(lib)} kernel {args.kernel} d={args.d} (stamps build {which}): {ms:.4f} ms/launch, "
+              f"in-kernel clock {clk:.3f} GHz, {np.median(ticks[ok] / fr[ok]):.0f} cycles per frame per wave (median)")
         rs = st[:, 0, 2 * SEGS + 4].astype(np.int64)
         re = st[:, 0, 2 * SEGS + 5].astype(np.int64)
-        hw = st[:, 0, 2 * SEGS + 6].astype(np.int64)
-        tg = (hw >> 16) & 15
         t0 = rs.min()
         rs_us, re_us = (rs - t0) * 0.01, (re - t0) * 0.01
         print(f"  workgroup start (us after the first): p50 {np.median(rs_us):.2f} max {rs_us.max():.2f}; "
               f"end: min {re_us.min():.1f} p10 {np.percentile(re_us, 10):.1f} p50 {np.median(re_us):.1f} "
               f"p90 {np.percentile(re_us, 90):.1f} max {re_us.max():.1f}")
-        for s_ in range(4):
-            m = tg == s_
-            if m.any():
-                print(f"    CU slot (HW_ID tg_id) {s_}: {m.sum():4d} workgroups, end p50 {np.median(re_us[m]):.1f} us, "
-                      f"min {re_us[m].min():.1f} max {re_us[m].max():.1f}")
-        # which SIMD each wave index of a workgroup runs on (HW_ID SIMD_ID, bits 5:4), and, over the
-        # workgroups sharing a CU (SE, SH, CU ids), whether wave 0 of every workgroup lands on one SIMD
-        hwa = st[:, :, 2 * SEGS + 6].astype(np.int64)
-        simd = (hwa >> 4) & 3
-        for wv in range(4):
-            cnt = np.bincount(simd[:, wv], minlength=4)
-            print(f"    wave {wv}: SIMD histogram {cnt.tolist()}")
-        cu = (hwa[:, 0] >> 8) & 0x7F   # CU_ID, SH_ID, SE_ID
-        same = []
-        for c in np.unique(cu):
-            m = cu == c
-            same.append(len(np.unique(simd[m, 0])))
-        print(f"    distinct SIMDs holding wave 0 among the workgroups of one CU id: "
-              f"{np.bincount(np.array(same), minlength=5)[1:].tolist()} (count of CU ids with 1, 2, 3, 4)")
-        lo = 4 if which >= 2 else 0
-        if which == 3:
-            for i, what in enumerate(("resolve", "s_next write", "next ticket", "ticket read (frame top)")):
-                qwk = [np.mean(st[:, w, i][ok[:, w]] / fr[:, w][ok[:, w]]) for w in range(4)]
-                print(f"  queue wave, inside seg 5: {what:36s} work " + " ".join(f"{x:7.0f}" for x in qwk))
+        print(f"  frames per workgroup: min {fr[:, 0].min():.0f} p50 {np.median(fr[:, 0]):.0f} max {fr[:, 0].max():.0f}")
+        lo = 4 * (which - 1)
         rows = []
         for i in range(SEGS):
             stamped = (lo <= i < lo + 4) or i == SEGS - 1
-            if not stamped:
+            if not stamped or work[i] == "-" and i != SEGS - 1:
                 continue
             wk = [np.mean(st[:, w, i][ok[:, w]] / fr[:, w][ok[:, w]]) for w in range(4)]
             wt = [np.mean(st[:, w, SEGS + i][ok[:, w]] / fr[:, w][ok[:, w]]) for w in range(4)] if i < SEGS - 1 else [0] * 4
-            name = WORK[i] if i == lo or i == SEGS - 1 or i > lo else WORK[i]
+            name = work[i]
             if i == lo and lo:
-                name = "frame start .. " + WORK[i] + " (incl. unstamped barriers 0..3)"
-            if i == SEGS - 1 and lo == 0:
-                name = "barrier 3 release .. frame end (incl. unstamped barriers 4..7)"
+                name = f"frame start .. {work[i]} (incl. unstamped barriers 0..{lo - 1})"
+            if i == SEGS - 1:
+                name = f"after barrier {lo + 3} .. frame end (incl. later unstamped barriers)"
             rows.append((i, name, wk, wt))
-            print(f"  seg {i}: {name:62s} work " + " ".join(f"{x:7.0f}" for x in wk)
+            print(f"  seg {i:2d}: {name:66s} work " + " ".join(f"{x:7.0f}" for x in wk)
                   + "   wait " + " ".join(f"{x:6.0f}" for x in wt))
-        res[os.path.basename(lib)] = {"ms": ms, "clock_GHz": clk, "build": which,
+        res[os.path.basename(lib)] = {"ms": ms, "clock_GHz": clk, "build": which, "kernel": args.kernel, "d": args.d,
+                                      "wg_end_us": {"min": float(re_us.min()), "p50": float(np.median(re_us)),
+                                                    "max": float(re_us.max())},
                                       "rows": [{"seg": i, "what": n, "work_cycles_per_frame_wave0..3": wk,
                                                 "barrier_wait_cycles_per_frame_wave0..3": wt}
                                                for i, n, wk, wt in rows]}

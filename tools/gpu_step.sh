@@ -1,0 +1,31 @@
+#!/bin/bash
+# One GPU-box session of steps, each under its own time limit, stopping at the first crash-like
+# exit (124/134/137/139): GPU tests (optional), an interleaved A/B of libraries, a bench line.
+#   tools/gpu_step.sh TAG [--tests] [--ab "ab_libs args"] [--bench] [--prof]
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$R"
+TAG=$1; shift
+O=$R/gpurun_out/$TAG; mkdir -p $O
+crashed() { case "$1" in 124|134|137|139) return 0;; *) return 1;; esac; }
+while [ $# -gt 0 ]; do
+  case "$1" in
+    --tests)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -q -rfE --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1
+      rc=$?; echo "pytest rc=$rc" >> $O/pytest_gpu.log; crashed $rc && exit $rc ;;
+    --testsel)
+      timeout -k 10 600 python -u -m pytest $2 -m gpu -q -rfE --timeout 200 --timeout-method thread > $O/pytest_sel.log 2>&1
+      rc=$?; echo "pytest rc=$rc" >> $O/pytest_sel.log; crashed $rc && exit $rc; shift ;;
+    --ab)
+      timeout -k 10 600 python -u tools/ab_libs.py $2 > $O/ab.log 2>&1
+      rc=$?; echo "ab rc=$rc" >> $O/ab.log; crashed $rc && exit $rc; shift ;;
+    --bench)
+      timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.log 2>&1
+      rc=$?; echo "bench rc=$rc" >> $O/bench.log; crashed $rc && exit $rc ;;
+    --prof)
+      (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python3 $R/bench.py --gpus 1 --steps 20 --warmup 5 > $O/trace.log 2>&1)
+      rc=$?; echo "prof rc=$rc" >> $O/trace.log; crashed $rc && exit $rc ;;
+  esac
+  shift
+done
+echo done > $O/DONE
