@@ -480,6 +480,9 @@ def main() -> None:
     ap.add_argument("--tunebin", type=int, default=1024)
     ap.add_argument("--nblk", type=int, default=2048, help="blocks of 65536 per step per GPU")
     ap.add_argument("--mode", choices=["single", "channels"], default="single")
+    ap.add_argument("--streams", type=int, default=1,
+                    help="single mode: consecutive batches alternate over this many HIP streams (each with its "
+                         "own output buffer), so one batch's launch tail overlaps the next batch's start")
     ap.add_argument("--channels", type=int, default=1024)
     ap.add_argument("--bcast", choices=["sag", "bcast"], default="sag",
                     help="C5 input broadcast for N > 1: scatter + all-gather over all links (sag) or one "
@@ -544,9 +547,29 @@ def main() -> None:
         d_in = make_input(torch, nblk, 0x5DDC, dev, first_block=rank * nblk)
         d_out = torch.empty(output_samples(d, nblk) * 2, dtype=out_dtype, device=dev)
         nch_local = 1
+        nstreams = max(1, args.streams)
+        # pipelined batches: step i on stream i % S into output S (the streams start behind `stream`
+        # and `stream` waits for all of them at the end of the timed region)
+        pstreams = [stream] + [torch.cuda.Stream(device=dev) for _ in range(nstreams - 1)]
+        pouts = [d_out] + [torch.empty_like(d_out) for _ in range(nstreams - 1)]
+        step_i = [0]
 
         def step():
-            ddc.process_device(d_in, nblk, d_out, stream)
+            i = step_i[0] % nstreams
+            step_i[0] += 1
+            ddc.process_device(d_in, nblk, pouts[i], pstreams[i])
+
+        def fork():   # the other streams start after the work queued on `stream`
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            for ps in pstreams[1:]:
+                ps.wait_event(ev)
+
+        def join():   # `stream` waits for the other streams
+            for ps in pstreams[1:]:
+                ev = torch.cuda.Event()
+                ev.record(ps)
+                stream.wait_event(ev)
         samples_per_step_all = nblk * BLOCK * world
         workload = f"single d={d} nblk={nblk}" + (f" fine_tune={args.fine_tune}" if args.fine_tune else "") \
             + (" cs16" if args.cs16 else "")
@@ -554,6 +577,13 @@ def main() -> None:
         ch = ChannelRun(torch, ddc, args.channels, nblk, d, out_dtype, dev, stream, world, rank, args.bcast)
         d_in, d_out, tbs, nch_local, step = ch.d_in, ch.d_out, ch.tbs, ch.nch_local, ch.step
         samples_per_step_all = nblk * BLOCK          # one shared stream
+        nstreams = 1
+
+        def fork():
+            pass
+
+        def join():
+            pass
         workload = f"channels d={d} nblk={nblk} nch={args.channels}" + (" cs16" if args.cs16 else "")
 
     tw0 = time.perf_counter()
@@ -584,15 +614,17 @@ def main() -> None:
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record(stream)
+    fork()
     for _ in range(args.steps):
         step()
+    join()
     ev1.record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    kern_ms = ev0.elapsed_time(ev1) / args.steps          # per step on the launch stream
+    kern_ms = ev0.elapsed_time(ev1) / args.steps          # per step on the launch stream(s)
     if args.mode == "channels":
         ch.close()                                        # waits for the prefetched broadcast
     t = torch.tensor([wall, kern_ms], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")

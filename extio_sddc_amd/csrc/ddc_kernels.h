@@ -75,9 +75,12 @@ struct KernelTables {
 hipError_t launch_frames_persistent(const KernelTables &t, int d, const int16_t *d_in, int nblk,
                                     void *d_out, const float4 *pq, int tunebin, int lsb, int rand,
                                     int cs16, float cs16_scale, const float2 *nco_starts,
-                                    const float2 *nco_trig, unsigned *wq, int static_pct, int device,
-                                    hipStream_t s);
+                                    const float2 *nco_trig, unsigned *wq, int static_pct, int tailwave,
+                                    int device, hipStream_t s);
 constexpr int kPStaticPct[7] = {75, 75, 75, 75, 75, 75, 75};
+// tailwave (d >= 3): the five-wave kernel whose fifth wave runs the inverse tail of the previous
+// frame (r2iq_tailwave_kernel); 0: the four-wave persistent kernel.  kPTailwave by default.
+constexpr int kPTailwave = 1;
 hipError_t launch_build_split_filter(const KernelTables &t, int d, int tunebin, float4 *pq, hipStream_t s);
 
 // d = 0 fused-split kernel (ddc_fs.hip, FS): used when fs_path(d, tunebin) (d = 0, tunebin a

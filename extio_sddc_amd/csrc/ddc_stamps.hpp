@@ -47,7 +47,7 @@ constexpr int kStLo = 4 * (SDDC_STAMPS - 1);
 #define ST_WRITE(buf, wg, tid)                                                                       \
     do {                                                                                             \
         const unsigned long long st_r1 = __builtin_amdgcn_s_memrealtime();                          \
-        if (((tid) & 63) == 0) {                                                                     \
+        if (((tid) & 63) == 0 && (tid) < 256) {   /* waves 0..3 (a fifth wave is not recorded) */   \
             unsigned *o = (buf) + ((size_t)(wg) * 4 + ((tid) >> 6)) * kStampWords;                   \
             for (int i = 0; i < kStampSegs; i++) {                                                   \
                 o[i] = st_work[i];                                                                   \
