@@ -1,5 +1,5 @@
-// ddc_queue.hpp — dynamic frame distribution for the persistent single-channel kernels
-// (ddc_persistent.hip).
+// ddc_queue.hpp — frame distribution for the single-channel frame kernels (ddc_fs.hip,
+// ddc_persistent.hip): a static prefix per workgroup, then a dynamic queue.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -11,17 +11,16 @@ namespace {
 // the four workgroups of a CU finish far apart: the SIMDs arbitrate by age, so the first-
 // dispatched workgroup of a CU runs ~1.6x faster than the last, and the CU spends the last
 // ~40 % of the launch with 3, 2, then 1 workgroup resident (s_memtime / s_memrealtime stamps
-// by HW_ID slot, profiles/r03/stamps).  Frames are handed out one at a time instead: 8 shards
-// of consecutive frames (one counter each, on its own 64-B line; a workgroup starts on shard
-// blockIdx % 8 and moves on when it runs dry), so consecutive frames, which share 2048 input
-// samples, mostly stay in one XCD's L2.  The queue wave (SDDC_FS_QWAVE) reads a ticket at the
-// top of the frame after the one it was taken in, resolves it before inverse pass 1 (the frame
-// is needed there, for its input prefetch) and takes the next ticket right after.  A device-
-// scope atomic's value is waited for with vmcnt, in issue order with every other vector-memory
-// operation of the wave; waiting for it in the frame it was taken cost ~1800 cycles per frame
-// (profiles/r03/stamps/stamps_q.txt .. stamps_q18.txt trace the variants; A/B in profiles/r03/ab).
-// The queue's remaining cost is ~700 cycles of the queue wave per frame at inverse pass 0 (the
-// other waves wait for it at the next barrier), against the ~8 % the static split lost.
+// by HW_ID slot, profiles/r03/stamps).  The frames past each workgroup's static prefix are handed
+// out one at a time instead: 8 shards of consecutive frames (one counter each, on its own 64-B
+// line; a workgroup starts on shard blockIdx % 8 and moves on when it runs dry), so consecutive
+// frames, which share 2048 input samples, mostly stay in one XCD's L2.  The queue wave reads a
+// ticket at the top of the frame after the one it was taken in, resolves it where the kernel
+// needs the next frame (for its input prefetch) and takes the next ticket right after.  A
+// device-scope atomic's value is waited for with vmcnt, in issue order with every other vector-
+// memory operation of the wave; waiting for it in the frame it was taken cost ~1800 cycles per
+// frame (profiles/r03/stamps/stamps_q.txt .. stamps_q18.txt trace the variants; A/B in
+// profiles/r03/ab).
 // wq: this launch's slot of the handle's queue ring, zero at entry; the last workgroup to leave
 // clears it for the slot's next launch (the counters are touched only by device-scope atomics).
 constexpr int FS_SHARDS = 8;
@@ -66,7 +65,6 @@ struct FsQueue {
     int shn;        // shard of the pending ticket (8: every shard dry)
     int lo, cnt;    // first frame and size of that shard (cnt = 0 once every shard is dry)
     int tk;         // lane 0: the pending ticket
-    bool mine = true;   // false: a wave that runs the bookkeeping without a queue (its atomics out of range)
     int pv;         // its value, read by peek()
 
     __device__ __forceinline__ void init(unsigned *wq, int nframes_, int home, int grid_ = 0, int per_ = 1)
@@ -96,7 +94,7 @@ struct FsQueue {
     __device__ __forceinline__ void take()
     {
         const unsigned off = shn < FS_SHARDS ? 64u * (unsigned)((sh0 + shn) & (FS_SHARDS - 1)) : FS_OOB;
-        const unsigned voff = (threadIdx.x & 63) == 0 && mine ? off : FS_OOB;
+        const unsigned voff = (threadIdx.x & 63) == 0 ? off : FS_OOB;
         tk = __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(1, rq, voff, 0, 0);
     }
     // reads the pending ticket (waits for its atomic): at the top of a frame, where the wait is
@@ -104,14 +102,33 @@ struct FsQueue {
     // nothing reads the result soon (v_readfirstlane's SGPR feeding a scalar compare right away
     // stalled the queue wave ~500 cycles per frame at inverse pass 0, stamps_q15.txt)
     __device__ __forceinline__ void peek() { pv = __builtin_amdgcn_readfirstlane(tk); }
-    // the frame of the peeked ticket; a ticket past its shard's end moves on to the next shard
-    // and takes (and waits for) a new ticket there: this happens only as the queue runs out.
-    // -1 when every shard is dry.
+    // the frame of the peeked ticket, -1 when every shard is dry.  A ticket past its shard's end
+    // (this happens only as the queue runs out) scans all eight counters at once (lanes 0..7 add
+    // 0 to one counter each: one device-scope round trip) and moves to the first shard in walk
+    // order from home that still has frames, where it takes (and waits for) a new ticket; with
+    // none left it returns at once.  Walking the shards one atomic at a time instead cost every
+    // workgroup's last frame 7 serial round trips (~1.2 us each while the chip streams,
+    // MI355X_MICROARCH.md dequeue row) on the launch's critical tail.  The counters only grow
+    // (until the last workgroup has left), so a shard seen dry stays dry, and a ticket below its
+    // shard's size is a frame no other ticket maps to: every frame is taken exactly once
+    // (tests/test_queue_model.py restates this and drives it with random interleavings).
     __device__ __forceinline__ int resolve()
     {
         bool dry = pv >= cnt;
         while (__builtin_expect(dry && shn < FS_SHARDS, 0)) {
-            set_shard(shn + 1);
+            const int l = (int)(threadIdx.x & 63);
+            const unsigned voff = l < FS_SHARDS ? 64u * (unsigned)l : FS_OOB;
+            const int seen = __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(0, rq, voff, 0, 0);
+            unsigned rot = 0;   // bit k: shard home + k has frames left (scalar: one VGPR in flight)
+#pragma unroll
+            for (int k = 0; k < FS_SHARDS; k++) {
+                const int s = (sh0 + k) & (FS_SHARDS - 1);
+                const int left = fs_shard_lo(nframes, s + 1) - fs_shard_lo(nframes, s) -
+                                 (grid ? fs_shard_pre(nframes, grid, s, per) : 0);
+                if (__builtin_amdgcn_readlane(seen, s) < left) rot |= 1u << k;
+            }
+            set_shard(rot ? __builtin_ctz(rot) : FS_SHARDS);
+            if (!rot) break;
             take();
             pv = __builtin_amdgcn_readfirstlane(tk);
             dry = pv >= cnt;

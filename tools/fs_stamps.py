@@ -51,7 +51,7 @@ P_WORK = {
 }
 
 
-def run(lib: str, kernel: str, d: int, nblk: int, tb: int):
+def run(lib: str, kernel: str, d: int, nblk: int, tb: int, params=()):
     import torch
     from extio_sddc_amd._lib import SIGNATURES
     L = ctypes.CDLL(os.path.abspath(lib))
@@ -64,6 +64,9 @@ def run(lib: str, kernel: str, d: int, nblk: int, tb: int):
     assert L.sddc_ddc_create(1.0, 0, ctypes.byref(h)) == 0
     L.sddc_ddc_set_tunebin(h, tb)
     L.sddc_ddc_set_decimation(h, d)
+    for k, v in params:   # sddc_ddc_internal_set_param (e.g. 3=0: the four-wave kernel at d >= 3)
+        L.sddc_ddc_internal_set_param.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+        assert L.sddc_ddc_internal_set_param(h, k, v) == 0
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(0x5DDC)
     d_in = torch.randint(-32768, 32767, (4096 + nblk * 65536,), dtype=torch.int16, device=dev, generator=g)
@@ -98,11 +101,13 @@ def main():
     ap.add_argument("--d", type=int, default=0)
     ap.add_argument("--nblk", type=int, default=2048)
     ap.add_argument("--tunebin", type=int, default=1024)
+    ap.add_argument("--param", action="append", default=[], help="PARAM=VALUE (sddc_ddc_internal_set_param)")
     args = ap.parse_args()
+    params = [tuple(int(v) for v in kv.split("=")) for kv in args.param]
     work = FS_WORK if args.kernel == "fs" else P_WORK[min(args.d, 4) if args.d >= 2 else 1]
     res = {}
     for lib in args.libs:
-        ms, st = run(lib, args.kernel, args.d, args.nblk, args.tunebin)
+        ms, st = run(lib, args.kernel, args.d, args.nblk, args.tunebin, params)
         which = int(st[0, 0, 2 * SEGS + 3])
         fr = st[:, :, 2 * SEGS].astype(np.float64)
         ok = fr > 0
