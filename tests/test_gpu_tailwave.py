@@ -2,7 +2,10 @@
 four-wave persistent kernel and the f64 oracle (pytest -m gpu).
 
 Both kernels compute the same frame (Core/fft_mt_r2iq_impl.hpp:84-138) with the same operations in
-the same order, so their outputs must be bit-identical; each is also held to 1e-5 of the oracle.
+the same order; each is held to 1e-5 of the oracle, and at d >= 4 they are bit-identical.  At d = 3
+(radix-8 tail passes with twiddles) the compiler contracts the tail's multiply-adds differently in
+the two kernels, so there they agree to float32 rounding (max |a - b| <= 1e-6 max |b|) rather than
+bit for bit.
 The tail wave works one frame behind the others and has its own final pass after the frame loop,
 so the cases include one-block batches, batches with fewer frames than workgroups, a 256-block
 batch through the frame queue, and the output stage's variants (sideband, rand, CS16, fused NCO).
@@ -75,10 +78,14 @@ def test_tailwave_equals_persistent_and_oracle(oracle, d, tb, lsb, rand, src, nb
             ys.append(_run(r, x, nblk, d))
     for y in ys:
         assert np.all(np.isfinite(y)), "samples never written"
-    np.testing.assert_array_equal(ys[0].view(np.uint32), ys[1].view(np.uint32))
     if src != "bench":   # (the bench tone tuned far away is a leakage-only channel: test_gpu_floor.py)
         ref = oracle.r2iq(x, nblk, d, tb, lsb, rand)
-        assert oracle.max_rel_err(ys[0], ref) <= TOL
+        errs = [oracle.max_rel_err(y, ref) for y in ys]
+        assert max(errs) <= TOL, errs
+    if d >= 4:
+        np.testing.assert_array_equal(ys[0].view(np.uint32), ys[1].view(np.uint32))
+    else:
+        assert np.max(np.abs(ys[0] - ys[1])) <= 1e-6 * np.max(np.abs(ys[1]))
 
 
 @pytest.mark.parametrize("d", [3, 4, 5, 6])
@@ -107,5 +114,10 @@ def test_tailwave_output_stage_variants(d):
             r.setFineTune(0.0)
             outs[on] = (y, c, m)
     for a, b in zip(outs[True], outs[False]):
-        np.testing.assert_array_equal(a.view(np.uint32) if a.dtype != np.int16 else a,
-                                      b.view(np.uint32) if b.dtype != np.int16 else b)
+        if d >= 4:
+            np.testing.assert_array_equal(a.view(np.uint32) if a.dtype != np.int16 else a,
+                                          b.view(np.uint32) if b.dtype != np.int16 else b)
+        elif a.dtype == np.int16:   # CS16: rounding differences move a sample by at most 1 LSB
+            assert np.max(np.abs(a.astype(np.int32) - b.astype(np.int32))) <= 1
+        else:
+            assert np.max(np.abs(a - b)) <= 1e-6 * np.max(np.abs(b))
