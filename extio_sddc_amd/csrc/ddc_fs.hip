@@ -395,7 +395,7 @@ hipError_t launch_fs_v(const KernelTables &t, const int16_t *d_in, int nblk, voi
     const int nframes = nblk * FRAMES;
     int grid = cus * occ;
     if (grid > nframes) grid = nframes;
-    const int kstat = frame_schedule_kstat(nframes, grid, static_pct);
+    const int kstat = frame_schedule_kstat(nframes, grid, static_pct, 1);
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), 0, s, reinterpret_cast<const int *>(d_in), d_out, nframes,
                        t.tw_p1, t.rec_f, pqf, fsl, tunebin, oa, nco, wq, kstat);
     return hipGetLastError();

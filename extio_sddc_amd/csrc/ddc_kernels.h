@@ -70,17 +70,10 @@ struct KernelTables {
 // nco_starts/nco_trig: fused fine-tune NCO tables (fine_tune.h), or nullptr for none.
 // cs16: write saturate(rint(x * cs16_scale)) int16 (I, Q) pairs instead of complex float.
 // wq: a zeroed dynamic-frame-queue slot (kFsQueueWords unsigned words), left zeroed.
-// static_pct: the share (percent) of each workgroup's frames taken statically before it draws
-// from the queue (ddc_queue.hpp FrameSchedule); kPStaticPct[d] by default.
 hipError_t launch_frames_persistent(const KernelTables &t, int d, const int16_t *d_in, int nblk,
                                     void *d_out, const float4 *pq, int tunebin, int lsb, int rand,
                                     int cs16, float cs16_scale, const float2 *nco_starts,
-                                    const float2 *nco_trig, unsigned *wq, int static_pct, int tailwave,
-                                    int device, hipStream_t s);
-constexpr int kPStaticPct[7] = {75, 75, 75, 75, 75, 75, 75};
-// tailwave (d >= 3): the five-wave kernel whose fifth wave runs the inverse tail of the previous
-// frame (r2iq_tailwave_kernel); 0: the four-wave persistent kernel.  kPTailwave by default.
-constexpr int kPTailwave = 1;
+                                    const float2 *nco_trig, unsigned *wq, int device, hipStream_t s);
 hipError_t launch_build_split_filter(const KernelTables &t, int d, int tunebin, float4 *pq, hipStream_t s);
 
 // d = 0 fused-split kernel (ddc_fs.hip, FS): used when fs_path(d, tunebin) (d = 0, tunebin a
@@ -94,7 +87,7 @@ hipError_t launch_build_fs_tables(const KernelTables &t, int tunebin, float4 *pq
 // static_pct: the share (percent) of each workgroup's frames taken statically before it draws
 // from the queue (ddc_queue.hpp FrameSchedule); kFsStaticPct by default.
 constexpr int kFsQueueWords = 16 * 9;
-constexpr int kFsStaticPct = 75;
+constexpr int kFsStaticPct = 40;
 hipError_t launch_frames_fs(const KernelTables &t, const int16_t *d_in, int nblk, void *d_out, const float4 *pqf,
                             const float2 *fsl, int tunebin, int lsb, int rand, int cs16, float cs16_scale,
                             const float2 *nco_starts, const float2 *nco_trig, unsigned *wq, int static_pct,

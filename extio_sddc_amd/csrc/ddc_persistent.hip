@@ -154,47 +154,12 @@ __device__ __forceinline__ void tail_pass(float2 *sb, const float2 *twq, int t, 
     }
 }
 
-// tail_pass with its twiddles W_{R NS}^{k r} read from the global 4096-point table (L1/L2
-// resident) instead of an LDS table: the tail-wave kernel's fifth wave has the issue slots and
-// the latency to spare, and the LDS the room for sb
-template <int N, int P>
-__device__ __forceinline__ void tail_pass_g(float2 *sb, __amdgpu_buffer_rsrc_t rtw, int t, float2 (&u)[8])
-{
-    constexpr int R = tail_radix<N>(P), NS = tail_ns<N>(P), T = N / R;
-    const int kk = t & (NS - 1);
-    if (t < T) {
-        float2 w[R];
-        if constexpr (P > 0) {
-#pragma unroll
-            for (int r = 1; r < R; r++)
-                w[r] = buf_load8(rtw, 8u * (unsigned)((kk * r * (HALF / (R * NS))) & (HALF - 1)), 0);
-        }
-        float2 a[R];
-#pragma unroll
-        for (int r = 0; r < R; r++) a[r] = sb[tail_swz<N>(t + T * r)];
-        if constexpr (P > 0) {
-#pragma unroll
-            for (int r = 1; r < R; r++) a[r] = TW<+1>(a[r], w[r]);
-        }
-        if constexpr (R == 8) dft8<+1>(a, u);
-        else dft4<+1>(a, u);
-    }
-    if constexpr (P + 1 < tail_passes<N>()) {
-        wave_lds_sync();   // this wave's reads of the pass are done
-        if (t < T) {
-#pragma unroll
-            for (int r = 0; r < R; r++) sb[tail_swz<N>((t / NS) * R * NS + kk + NS * r)] = u[r];
-        }
-        wave_lds_sync();
-    }
-}
-
 template <int D, bool RAND, bool NCO, bool CS16>
 __global__ __launch_bounds__(NT, 4) void r2iq_persistent_kernel(
     const int *__restrict__ in32, void *__restrict__ out, int nframes,
     const float2 *__restrict__ tw_p1, const float2 *__restrict__ tw_q1,
     const float2 *__restrict__ rec_f, const float2 *__restrict__ rec_i, const float2 *__restrict__ tw4096,
-    const float4 *__restrict__ pq, int tunebin, OutArgs oa, NcoArgs nco, unsigned *__restrict__ wq, int kstat)
+    const float4 *__restrict__ pq, int tunebin, OutArgs oa, NcoArgs nco, unsigned *__restrict__ wq)
 {
     constexpr int N = HALF >> D;
     // d >= 2 (N <= 1024): the inverse reads only the band [s0, s0 + N) of Z and its mirror
@@ -258,17 +223,42 @@ __global__ __launch_bounds__(NT, 4) void r2iq_persistent_kernel(
 
     const int tid = (int)threadIdx.x;
     const int G = (int)gridDim.x, w = (int)blockIdx.x;
-    // Frames come from the static-prefix + dynamic-suffix schedule (ddc_queue.hpp FrameSchedule),
-    // worked by wave 3: the frame after the next one is learnt in the middle of each frame (the
-    // next one's input is prefetched at the frame's start), from a ticket taken a frame earlier
-    // once the workgroup's static frames run out.
+    // d <= 2: frames come from the dynamic frame queue (ddc_queue.hpp), worked by wave 3, after
+    // two static frames per workgroup (fs_static_frame: no atomic round trip before the first
+    // frames): the frame after the next one is learnt in the middle of each frame (the next one's
+    // input is prefetched at the frame's start), from a ticket taken a frame earlier.  d = 1 +4 %, d = 2 +1 % against a
+    // static split, but d = 3 -2 % and d = 4 -4 % (their frames are short and the queue wave's
+    // bookkeeping is not), so d >= 3 keep the static contiguous split (profiles/r03/ab/
+    // pq_dynamic_queue_d1_4.txt, p_queue_d3_6_after_tails.txt; round 4 re-measured a static prefix
+    // of 75 % at every d: d = 3, 4 -4 %, d = 1, 2 -1 to -2 %, profiles/r04/ab).
+    constexpr bool PQ = D <= 2;
     __shared__ int s_first, s_next;
     constexpr int QLANE = 64 * 3;
     const bool qw = __builtin_amdgcn_readfirstlane(tid >> 6) == 3;
-    FrameSchedule<2> fsch;
+    const int f1s = (int)(((long long)nframes * (w + 1)) / G);   // the static split's range end
+    FsQueue<-1> q;   // (the FrameSchedule's extra scalar state spilled 19-27 SGPRs at d = 2)
+    if constexpr (PQ) q.init(wq, nframes, w & (FS_SHARDS - 1), G, 2);
     if (qw) {
         int g[2];
-        fsch.init(wq, nframes, w, G, kstat, g);
+        if constexpr (PQ) {
+            g[0] = fs_static_frame(nframes, G, w, 0, 2);
+            g[1] = fs_static_frame(nframes, G, w, 1, 2);
+            if (g[0] < 0) {   // no static frames (small batches): both from the queue
+                q.take();
+                q.peek();
+                g[0] = q.resolve();
+            }
+            if (g[1] < 0) {
+                q.take();
+                q.peek();
+                g[1] = g[0] >= 0 ? q.resolve() : -1;
+            }
+            q.take();
+        } else {
+            const int f0 = (int)(((long long)nframes * w) / G);
+            g[0] = f0 < f1s ? f0 : -1;
+            g[1] = f0 + 1 < f1s ? f0 + 1 : -1;
+        }
         if (tid == QLANE) {
             s_first = g[0];
             s_next = g[1];
@@ -393,9 +383,14 @@ __global__ __launch_bounds__(NT, 4) void r2iq_persistent_kernel(
             for (int r = 0; r < 16; r++) w0[sZ + NT * r] = v[r];   // Z, rotated by tb
         }
         if (qw) {   // the frame after the next one (read by every wave at the next frame's start)
-            fsch.peek();
-            const int g = fsch.next();
-            if (tid == QLANE) s_next = g;
+            if constexpr (PQ) {
+                q.peek();
+                const int g = q.resolve();
+                if (tid == QLANE) s_next = g;
+                q.take();
+            } else if (tid == QLANE) {
+                s_next = fn >= 0 && fn + 1 < f1s ? fn + 1 : -1;
+            }
         }
         ST_SYNC(5);
 
@@ -567,198 +562,8 @@ __global__ __launch_bounds__(NT, 4) void r2iq_persistent_kernel(
         f = fn;
     }
     ST_WRITE(g_p_stamps, w, tid);
-    if (tid == QLANE) fs_queue_done(wq, (unsigned)G);
-}
-
-// ---------------------------------------------------------------------------------------------
-// d = 3..6 (N = 512 .. 64): the tail-wave kernel.  In the persistent kernel above the inverse
-// tail (three or four Stockham passes on wave 0) and the IQ stores run between the split and the
-// next frame's first barrier, with the other three waves waiting for wave 0 at that barrier.  Here
-// a fifth wave (320 threads) owns the tail: while waves 0..3 run frame f's forward passes, wave 4
-// runs frame f - 1's inverse passes (one per barrier segment, on the filtered bins the split left
-// in sb) and stores its IQ, so the tail leaves the frame's critical path.  sb is free again
-// before frame f's split writes it (the passes end at barrier 3; the split starts after
-// barrier 5).  The tail's twiddles come from the global 4096-point table (tail_pass_g), so the
-// LDS holds the frame, the pass-1 table and sb only (38.8 KB at d = 3: 4 workgroups per CU).
-// VGPRs <= 96 for 5 waves per SIMD.
-template <int D, bool RAND, bool NCO, bool CS16>
-__global__ __launch_bounds__(NT + 64, 4) __attribute__((amdgpu_num_vgpr(96))) void r2iq_tailwave_kernel(
-    const int *__restrict__ in32, void *__restrict__ out, int nframes, const float2 *__restrict__ tw_p1,
-    const float2 *__restrict__ tw4096, const float4 *__restrict__ pq, int tunebin, OutArgs oa, NcoArgs nco,
-    unsigned *__restrict__ wq, int kstat)
-{
-    constexpr int N = HALF >> D;
-    static_assert(N >= 64 && N <= 512, "tail-wave kernel: d = 3..6");
-    constexpr int NB = N >= 512 ? N / 256 + 1 : 2;   // Z registers per thread in the band (and in the mirror)
-    const int s0 = (tunebin - N / 2) & (HALF - 1), r0 = s0 >> 8;
-    const int mrel = ((((1 - s0 - N) & (HALF - 1)) >> 8) - r0) & 15;
-    __shared__ __attribute__((aligned(16))) float2 lds[HALF];
-    __shared__ __attribute__((aligned(16))) float2 twl[15 * 16];   // pass-1 twiddles W_256^{s r}
-    __shared__ __attribute__((aligned(16))) float2 sb[N];
-    __shared__ int s_first, s_next;
-
-    const int tid = (int)threadIdx.x;
-    const int G = (int)gridDim.x, w = (int)blockIdx.x;
-    const bool tw = __builtin_amdgcn_readfirstlane(tid >> 6) == 4;   // the tail wave
-    constexpr int QLANE = 64 * 3;
-    const bool qw = __builtin_amdgcn_readfirstlane(tid >> 6) == 3;
-    FrameSchedule<2> fsch;
-    if (qw) {
-        int g[2];
-        fsch.init(wq, nframes, w, G, kstat, g);
-        if (tid == QLANE) {
-            s_first = g[0];
-            s_next = g[1];
-        }
-    }
-    // forward pass-2 bases rotated by 256 r0 (the band in registers 0 .. NB - 1, the mirror in
-    // mrel ..)
-    const int tt = tid & (NT - 1);
-    const float2 fw1_ = tw4096[(tt + 256 * r0) & (HALF - 1)];
-    const float2 fw4_ = tw4096[(4 * tt + 1024 * r0) & (HALF - 1)];
-    for (int i = tid; i < 15 * 16; i += NT + 64) twl[i] = tw_p1[i];
-
-    __syncthreads();   // s_first, s_next
-    int f = s_first;
-    ST_INIT();
-    // Two disjoint loops, one per role, each passing the same 7 barriers per frame (s_barrier
-    // counts waves, and every wave is uniform in its role): the registers of the FFT waves' loop
-    // are not reserved around the tail wave's code and vice versa.
-    if (tw) {
-        // ---- the tail wave: frame f - 1's inverse passes, one per segment, then its IQ ----
-        int fprev = -1;
-        while (f >= 0) {
-            const int fn = s_next;
-            const int pblk = fprev / FRAMES, pk = fprev - pblk * FRAMES;
-            // opaque per-frame copies: without them the compiler hoists the (loop-invariant) twiddle
-            // loads out of the frame loop and keeps them live in VGPRs
-            int z = 0;
-            asm volatile("" : "+s"(z));
-            const int tl = tid - NT + z;
-            const __amdgpu_buffer_rsrc_t rtw = buf_rsrc(tw4096 + z);
-            if (fprev >= 0) {
-                float2 u[8];
-                tail_pass_g<N, 0>(sb, rtw, tl, u);
-            }
-            ST_SYNC(0);
-            if (fprev >= 0) {
-                float2 u[8];
-                tail_pass_g<N, 1>(sb, rtw, tl, u);
-            }
-            ST_SYNC(1);
-            if (fprev >= 0) {
-                float2 u[8];
-                tail_pass_g<N, 2>(sb, rtw, tl, u);
-                if constexpr (tail_passes<N>() == 3)
-                    tail_emit<N, NCO, CS16>(out, pblk * 8 * N + emit_base<N>(pk), pk, tl, u, oa, nco);
-            }
-            ST_SYNC(2);
-            if constexpr (tail_passes<N>() == 4) {
-                if (fprev >= 0) {
-                    float2 u[8];
-                    tail_pass_g<N, 3>(sb, rtw, tl, u);
-                    tail_emit<N, NCO, CS16>(out, pblk * 8 * N + emit_base<N>(pk), pk, tl, u, oa, nco);
-                }
-            }
-            ST_SYNC(3);   // sb is free for this frame's split (after barrier 5)
-            ST_SYNC(4);
-            ST_SYNC(5);
-            ST_SYNC(6);   // this frame's filtered bins are in sb
-            ST_FRAME_END();
-            fprev = f;
-            f = fn;
-        }
-        if (fprev >= 0) {   // the last frame's tail
-            const int tl = tid - NT;
-            const __amdgpu_buffer_rsrc_t rtw = buf_rsrc(tw4096);
-            const int pblk = fprev / FRAMES, pk = fprev - pblk * FRAMES;
-            float2 u[8];
-            tail_pass_g<N, 0>(sb, rtw, tl, u);
-            tail_pass_g<N, 1>(sb, rtw, tl, u);
-            tail_pass_g<N, 2>(sb, rtw, tl, u);
-            if constexpr (tail_passes<N>() == 4) tail_pass_g<N, 3>(sb, rtw, tl, u);
-            tail_emit<N, NCO, CS16>(out, pblk * 8 * N + emit_base<N>(pk), pk, tl, u, oa, nco);
-        }
-    } else {
-        // ---- the FFT waves: forward passes, Z, split x filter into sb ----
-        int x[16];
-        if (f >= 0) load_frame(in32, f / FRAMES, f - (f / FRAMES) * FRAMES, x);
-        while (f >= 0) {
-            const int fn = s_next;   // the next frame (learnt in the previous frame's middle)
-            int z = 0;
-            asm volatile("" : "+s"(z));
-            const int t = tid + z;
-            const float4 *pqz = pq + z;
-            float2 fw1 = fw1_, fw4 = fw4_;
-            asm volatile("" : "+v"(fw1), "+v"(fw4));
-            const int sT = swz(t);
-            const int x15 = t & 15;
-            const unsigned xa0 = 128u * (unsigned)t + 8u * (unsigned)x15;
-            const unsigned xa1 = 2048u * (unsigned)(t >> 4) + 8u * (unsigned)x15;
-            float2 v[16];
-            {   // F0: convert (+ rand), prefetch, DFT16
-                float2 a[16];
-#pragma unroll
-                for (int r = 0; r < 16; r++)
-                    if constexpr (RAND) {
-                        const int wd = x[r] ^ (int)(((unsigned)x[r] & 0x10001u) * 0xFFFEu);   // fft_mt_r2iq.h:36-51
-                        a[r] = make_float2((float)(int)(short)(wd & 0xffff), (float)(wd >> 16));
-                    } else {
-                        a[r] = make_float2((float)(int)(short)(x[r] & 0xffff), (float)(x[r] >> 16));
-                    }
-                if (fn >= 0) load_frame(in32, fn / FRAMES, fn - (fn / FRAMES) * FRAMES, x);
-                dft16<-1>(a, v);
-            }
-            ST_SYNC(0);   // the previous frame's Z reads are done
-#pragma unroll
-            for (int r = 0; r < 16; r++) st_row(lds, xa0, r, 0, v[r]);
-            ST_SYNC(1);
-            {   // F1: twiddles W_256^{(t%16) r}, DFT16
-                float2 a[16];
-#pragma unroll
-                for (int r = 0; r < 16; r++) XRD(a[r], lds[sT + NT * r]);
-                table_twiddle<-1, false>(a, twl, 16, x15);
-                dft16<-1>(a, v);
-            }
-            ST_SYNC(2);
-#pragma unroll
-            for (int r = 0; r < 16; r++) st_row(lds, xa1, r, 16, v[r]);
-            ST_SYNC(3);
-            {   // F2: recurrence twiddles W_4096^{(t + 256 r0) r}, DFT16
-                float2 a[16];
-#pragma unroll
-                for (int r = 0; r < 16; r++) XRD(a[r], lds[sT + NT * r]);
-                twiddle_rec16<-1>(a, fw1, fw4);
-                dft16<-1>(a, v);
-            }
-            ST_SYNC(4);
-#pragma unroll
-            for (int r = 0; r < 16; r++)   // Z: the band's and the mirror's registers only
-                if (r < NB || ((r - mrel) & 15) < NB) lds[t + NT * ((r + r0) & 15)] = v[r];
-            if (qw) {   // the frame after the next one
-                fsch.peek();
-                const int g = fsch.next();
-                if (tid == QLANE) s_next = g;
-            }
-            ST_SYNC(5);
-            {   // split x filter: the N filtered bins to sb (tail_swz order)
-                constexpr int PER = N > NT ? N / NT : 1;
-#pragma unroll
-                for (int i = 0; i < PER; i++) {
-                    const int m = t + NT * i;
-                    if (m < N) {
-                        const int bin = tunebin + m - (m >= N / 2 ? N : 0);
-                        sb[tail_swz<N>(m)] = split_pq(lds[bin & (HALF - 1)], lds[(HALF - bin) & (HALF - 1)], pqz[m]);
-                    }
-                }
-            }
-            ST_SYNC(6);
-            ST_FRAME_END();
-            f = fn;
-        }
-    }
-    ST_WRITE(g_p_stamps, w, tid);
-    if (tid == QLANE) fs_queue_done(wq, (unsigned)G);
+    if constexpr (PQ)
+        if (tid == QLANE) fs_queue_done(wq, (unsigned)G);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -796,8 +601,6 @@ struct Launch {
     OutArgs oa;
     NcoArgs nco;
     unsigned *wq;   // a zeroed dynamic-frame-queue slot (kFsQueueWords)
-    int static_pct; // the frame schedule's static share (ddc_queue.hpp)
-    bool tailwave;  // d >= 3: the tail-wave kernel
 };
 
 template <int D, bool RAND, bool NCO, bool CS16>
@@ -812,31 +615,13 @@ hipError_t launch_v(const KernelTables &t, const Launch &L)
     if (grid > nframes) grid = nframes;
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), 0, L.s, reinterpret_cast<const int *>(L.d_in),
                        L.d_out, nframes, t.tw_p1, t.tw_q1[D], t.rec_f, t.rec_i[D], t.tw4096, L.pq, L.tunebin, L.oa,
-                       L.nco, L.wq, frame_schedule_kstat(nframes, grid, L.static_pct));
-    return hipGetLastError();
-}
-
-template <int D, bool RAND, bool NCO, bool CS16>
-hipError_t launch_tw(const KernelTables &t, const Launch &L)
-{
-    auto kern = r2iq_tailwave_kernel<D, RAND, NCO, CS16>;
-    int occ = 0, cus = 0;
-    hipError_t e = launch_geometry(t.lc, reinterpret_cast<const void *>(kern), NT + 64, L.device, &occ, &cus);
-    if (e != hipSuccess) return e;
-    const int nframes = L.nblk * FRAMES;
-    int grid = cus * occ;
-    if (grid > nframes) grid = nframes;
-    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT + 64), 0, L.s, reinterpret_cast<const int *>(L.d_in),
-                       L.d_out, nframes, t.tw_p1, t.tw4096, L.pq, L.tunebin, L.oa, L.nco, L.wq,
-                       frame_schedule_kstat(nframes, grid, L.static_pct));
+                       L.nco, L.wq);
     return hipGetLastError();
 }
 
 template <int D, bool RAND, bool NCO>
 hipError_t launch_f(const KernelTables &t, const Launch &L, bool cs16)
 {
-    if constexpr (D >= 3)
-        if (L.tailwave) return cs16 ? launch_tw<D, RAND, NCO, true>(t, L) : launch_tw<D, RAND, NCO, false>(t, L);
     return cs16 ? launch_v<D, RAND, NCO, true>(t, L) : launch_v<D, RAND, NCO, false>(t, L);
 }
 
@@ -861,12 +646,11 @@ hipError_t launch_build_split_filter(const KernelTables &t, int d, int tunebin, 
 
 hipError_t launch_frames_persistent(const KernelTables &t, int d, const int16_t *d_in, int nblk, void *d_out,
                                     const float4 *pq, int tunebin, int lsb, int rand, int cs16, float cs16_scale,
-                                    const float2 *nco_starts, const float2 *nco_trig, unsigned *wq, int static_pct,
-                                    int tailwave, int device, hipStream_t s)
+                                    const float2 *nco_starts, const float2 *nco_trig, unsigned *wq, int device,
+                                    hipStream_t s)
 {
-    if (static_pct < 0 || static_pct > 100) return hipErrorInvalidValue;
     const Launch L{d_in, nblk, d_out, pq, tunebin, device, s, OutArgs{lsb ? 0x80000000u : 0u, cs16_scale},
-                   NcoArgs{nco_starts, nco_trig}, wq, static_pct, tailwave != 0};
+                   NcoArgs{nco_starts, nco_trig}, wq};
     const bool f = cs16 != 0;
     switch (d) {
     case 0: return launch_d<0>(t, L, rand, f);

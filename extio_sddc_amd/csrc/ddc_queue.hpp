@@ -59,15 +59,33 @@ __device__ __forceinline__ int fs_static_frame(int nframes, int grid, int w, int
     return e < fs_shard_pre(nframes, grid, s, per) ? fs_shard_lo(nframes, s) + e : -1;
 }
 __device__ __forceinline__ int fs_static_first(int nframes, int grid, int w) { return fs_static_frame(nframes, grid, w, 0, 1); }
+// Pair tickets (kTailSingles >= 0): the first tickets of a shard stand for two consecutive frames
+// each, the last ones (kTailSingles per workgroup homed there) for one.  A workgroup then dequeues about
+// once per two frames (each dequeue is ~1000 cycles of the queue wave that the other waves wait
+// for at the next barrier, profiles/r03/stamps), and the queue still ends in single frames, so
+// the launch's tail keeps the granularity of one frame.  Shard s's dynamic frames (past its static
+// prefix) are lo_s + [0, 2 np_s) in pairs (ticket t: lo_s + 2t, lo_s + 2t + 1) and lo_s + 2 np_s ..
+// one per ticket (ticket t >= np_s: lo_s + np_s + t); its tickets number cnt_s - np_s.
+// TS < 0: every ticket one frame.  kTailSingles: the d = 0 kernel's (FrameSchedule).
+constexpr int kTailSingles = -1;
+template <int TS>
+__device__ __forceinline__ int fs_shard_pairs(int cnt, int grid, int s)
+{
+    if constexpr (TS < 0) return 0;
+    const int n = TS * fs_shard_nwg(grid, s);
+    return cnt > n ? (cnt - n) >> 1 : 0;
+}
+template <int TS>
 struct FsQueue {
     __amdgpu_buffer_rsrc_t rq;   // the queue slot as a buffer (kFsQueueWords words)
     int nframes, sh0, grid, per;
     int shn;        // shard of the pending ticket (8: every shard dry)
-    int lo, cnt;    // first frame and size of that shard (cnt = 0 once every shard is dry)
+    int lo;         // first dynamic frame of that shard
+    int np, ntk;    // its pair tickets and all its tickets (ntk = 0 once every shard is dry)
     int tk;         // lane 0: the pending ticket
     int pv;         // its value, read by peek()
 
-    __device__ __forceinline__ void init(unsigned *wq, int nframes_, int home, int grid_ = 0, int per_ = 1)
+    __device__ __forceinline__ void init(unsigned *wq, int nframes_, int home, int grid_, int per_)
     {
         rq = __builtin_amdgcn_make_buffer_rsrc(wq, (short)0, 4 * kFsQueueWords, 0x00020000);
         nframes = nframes_;
@@ -76,17 +94,20 @@ struct FsQueue {
         per = per_;
         set_shard(0);
     }
+    // the dynamic frames of shard s (past its static prefix)
+    __device__ __forceinline__ int dyn(int s, int &first) const
+    {
+        const int pre = fs_shard_pre(nframes, grid, s, per);
+        first = fs_shard_lo(nframes, s) + pre;
+        return fs_shard_lo(nframes, s + 1) - first;
+    }
     __device__ __forceinline__ void set_shard(int sh)
     {
         shn = sh;
         const int s = (sh0 + sh) & (FS_SHARDS - 1);
-        lo = fs_shard_lo(nframes, s);
-        cnt = sh < FS_SHARDS ? fs_shard_lo(nframes, s + 1) - lo : 0;
-        if (grid) {   // the static first frames
-            const int pre = fs_shard_pre(nframes, grid, s, per);
-            lo += pre;
-            cnt -= pre;
-        }
+        const int cnt = sh < FS_SHARDS ? dyn(s, lo) : 0;
+        np = fs_shard_pairs<TS>(cnt, grid, s);
+        ntk = cnt - np;
     }
     // takes a ticket of the current shard (lane 0; no wait).  Called by the whole wave; the
     // offset is recomputed here (a few scalar instructions and one select) rather than kept in
@@ -102,7 +123,8 @@ struct FsQueue {
     // nothing reads the result soon (v_readfirstlane's SGPR feeding a scalar compare right away
     // stalled the queue wave ~500 cycles per frame at inverse pass 0, stamps_q15.txt)
     __device__ __forceinline__ void peek() { pv = __builtin_amdgcn_readfirstlane(tk); }
-    // the frame of the peeked ticket, -1 when every shard is dry.  A ticket past its shard's end
+    // the frame of the peeked ticket (second: the pair's second frame, or -1), -1 when every shard
+    // is dry.  A ticket past its shard's end
     // (this happens only as the queue runs out) scans all eight counters at once (lanes 0..7 add
     // 0 to one counter each: one device-scope round trip) and moves to the first shard in walk
     // order from home that still has frames, where it takes (and waits for) a new ticket; with
@@ -114,26 +136,36 @@ struct FsQueue {
     // (tests/test_queue_model.py restates this and drives it with random interleavings).
     __device__ __forceinline__ int resolve()
     {
-        bool dry = pv >= cnt;
+        int second;
+        return resolve(second);
+    }
+    __device__ __forceinline__ int resolve(int &second)
+    {
+        bool dry = pv >= ntk;
         while (__builtin_expect(dry && shn < FS_SHARDS, 0)) {
             const int l = (int)(threadIdx.x & 63);
             const unsigned voff = l < FS_SHARDS ? 64u * (unsigned)l : FS_OOB;
             const int seen = __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(0, rq, voff, 0, 0);
-            unsigned rot = 0;   // bit k: shard home + k has frames left (scalar: one VGPR in flight)
+            unsigned rot = 0;   // bit k: shard home + k has tickets left (scalar: one VGPR in flight)
 #pragma unroll
             for (int k = 0; k < FS_SHARDS; k++) {
                 const int s = (sh0 + k) & (FS_SHARDS - 1);
-                const int left = fs_shard_lo(nframes, s + 1) - fs_shard_lo(nframes, s) -
-                                 (grid ? fs_shard_pre(nframes, grid, s, per) : 0);
-                if (__builtin_amdgcn_readlane(seen, s) < left) rot |= 1u << k;
+                int first;
+                const int cnt = dyn(s, first);
+                if (__builtin_amdgcn_readlane(seen, s) < cnt - fs_shard_pairs<TS>(cnt, grid, s)) rot |= 1u << k;
             }
             set_shard(rot ? __builtin_ctz(rot) : FS_SHARDS);
             if (!rot) break;
             take();
             pv = __builtin_amdgcn_readfirstlane(tk);
-            dry = pv >= cnt;
+            dry = pv >= ntk;
         }
-        return dry ? -1 : lo + pv;
+        if constexpr (TS < 0) {
+            second = -1;
+            return dry ? -1 : lo + pv;
+        }
+        second = !dry && pv < np ? lo + 2 * pv + 1 : -1;
+        return dry ? -1 : pv < np ? lo + 2 * pv : lo + np + pv;
     }
 };
 // Static prefix + dynamic suffix: each workgroup first takes kstat static frames of its home
@@ -152,54 +184,72 @@ struct FsQueue {
 // LA: lookahead, the number of frames known ahead of the current one (1: the FS kernel, which
 // learns frame j + 1 at frame j's inverse pass 0; 2: the persistent kernel, which prefetches
 // frame j + 1 at frame j's top and learns frame j + 2 in frame j's middle).
-template <int LA>
+template <int LA, int TS = kTailSingles>
 struct FrameSchedule {
-    FsQueue q;
-    int j = 0;      // index of the current frame in the workgroup's sequence
-    int kw = 0;     // this workgroup's static frames: slo + i nwg, i < kw
-    int slo, nwg;
+    FsQueue<TS> q;
+    int rem;        // static frames left past the LA known ones (<= 0: the rest is dynamic)
+    int nxt, nwg;   // the next of them, and the stride between them (static frame i: slo + i nwg)
+    int pend = -1;  // the second frame of the last pair ticket, not yet handed out
+    static constexpr bool PAIRS = TS >= 0;
 
-    // frame i < LA of the sequence: static, or from the queue at once (small batches)
-    __device__ __forceinline__ int first(int i)
-    {
-        if (i < kw) return slo + i * nwg;
-        q.take();
-        q.peek();
-        return q.resolve();
-    }
-    // sets up the schedule; f[0..LA) receive the first LA frames (-1: none)
+    // sets up the schedule; f[0..LA) receive the first LA frames (-1: none).  kstat: static frames
+    // per workgroup
     __device__ __forceinline__ void init(unsigned *wq, int nframes, int w, int grid, int kstat, int (&f)[LA])
     {
         const int s = w & (FS_SHARDS - 1);
         nwg = fs_shard_nwg(grid, s);
-        slo = fs_shard_lo(nframes, s) + w / FS_SHARDS;
+        const int slo = fs_shard_lo(nframes, s) + w / FS_SHARDS;
         const int pre = fs_shard_pre(nframes, grid, s, kstat);
-        kw = pre > w / FS_SHARDS ? (pre - w / FS_SHARDS + nwg - 1) / nwg : 0;
+        const int kw = pre > w / FS_SHARDS ? (pre - w / FS_SHARDS + nwg - 1) / nwg : 0;
         q.init(wq, nframes, s, grid, kstat);
-        for (int i = 0; i < LA; i++) f[i] = first(i);
-        if (LA >= kw) q.take();   // frame LA is dynamic: its ticket now
+        for (int i = 0; i < LA; i++) {   // frame i: static, or from the queue at once (small batches)
+            if (PAIRS && pend >= 0) {
+                f[i] = pend;
+                pend = -1;
+            } else if (i < kw) {
+                f[i] = slo + i * nwg;
+            } else {
+                q.take();
+                q.peek();
+                f[i] = q.resolve(pend);
+            }
+        }
+        rem = kw - LA;
+        nxt = slo + LA * nwg;
+        if (rem <= 0 && (!PAIRS || pend < 0)) q.take();   // frame LA is dynamic and not known: its ticket now
     }
     // reads the pending ticket, if any (taken a frame earlier): call at a point where its wait
     // is free, before next()
     __device__ __forceinline__ void peek()
     {
-        if (j + LA >= kw) q.peek();
+        if (rem <= 0 && (!PAIRS || pend < 0)) q.peek();
     }
-    // frame j + LA, and the ticket for frame j + LA + 1 when that one is dynamic; then j++
+    // the frame LA after the current one, and the ticket for the one after that when it is
+    // dynamic and not the second of a pair
     __device__ __forceinline__ int next()
     {
-        const int fn = j + LA < kw ? slo + (j + LA) * nwg : q.resolve();
-        if (j + LA + 1 >= kw) q.take();
-        j++;
+        int fn;
+        if (PAIRS && pend >= 0) {
+            fn = pend;
+            pend = -1;
+        } else if (rem > 0) {
+            fn = nxt;
+            nxt += nwg;
+        } else {
+            fn = q.resolve(pend);
+        }
+        rem--;
+        if (rem <= 0 && (!PAIRS || pend < 0)) q.take();
         return fn;
     }
 };
 
-// static frames per workgroup for a static share of pct percent (at least one)
-inline int frame_schedule_kstat(int nframes, int grid, int pct)
+// static frames per workgroup for a static share of pct percent, at least lo (the schedule's
+// lookahead: the frames a workgroup needs before its first ticket could have returned)
+inline int frame_schedule_kstat(int nframes, int grid, int pct, int lo)
 {
     const int k = (int)((long long)nframes * pct / (100LL * grid));
-    return k < 1 ? 1 : k;
+    return k < lo ? lo : k;
 }
 
 __device__ __forceinline__ void fs_queue_done(unsigned *wq, unsigned grid)

@@ -232,10 +232,6 @@ struct sddc_ddc {
     unsigned *d_queue = nullptr;
     int queue_slot = 0;
     int fs_static_pct = sddc::kFsStaticPct;   // the d = 0 kernel's static share of frames (ddc_queue.hpp)
-    int p_static_pct[SDDC_DDC_NDEC] = {sddc::kPStaticPct[0], sddc::kPStaticPct[1], sddc::kPStaticPct[2],
-                                       sddc::kPStaticPct[3], sddc::kPStaticPct[4], sddc::kPStaticPct[5],
-                                       sddc::kPStaticPct[6]};   // the persistent kernel's, per d
-    int p_tailwave = sddc::kPTailwave;        // d >= 3: the tail-wave kernel
     hipStream_t q_s[kQueueSlots] = {};
     bool q_used[kQueueSlots] = {};
     bool q_dirty[kQueueSlots] = {};
@@ -769,7 +765,7 @@ static hipError_t launch_single_impl(sddc_ddc_t *h, const int16_t *d_in, int nbl
                                         h->device, s)
         : sddc::launch_frames_persistent(h->tables, h->d, d_in, nblk, d_out, h->d_pq, h->tunebin, h->lsb, h->rand,
                                          h->out_fmt == SDDC_DDC_FMT_CS16, h->cs16_scale, nco_starts, nco_trig,
-                                         wq, h->p_static_pct[h->d], h->p_tailwave, h->device, s);
+                                         wq, h->device, s);
     if (qi >= 0) queue_slot_launched(h, qi, s, e);
     if (e != hipSuccess) return e;
     return h->readers.record(s);
@@ -821,13 +817,6 @@ int sddc_ddc_internal_set_param(sddc_ddc_t *h, int param, int value)
     case SDDC_DDC_PARAM_FS_STATIC_PCT:
         if (value < 0 || value > 100) return fail(SDDC_ERR_ARG, "static share %d outside 0..100", value);
         h->fs_static_pct = value;
-        return SDDC_OK;
-    case SDDC_DDC_PARAM_P_STATIC_PCT:
-        if (value < 0 || value > 100) return fail(SDDC_ERR_ARG, "static share %d outside 0..100", value);
-        for (int &v : h->p_static_pct) v = value;
-        return SDDC_OK;
-    case SDDC_DDC_PARAM_P_TAILWAVE:
-        h->p_tailwave = value != 0;
         return SDDC_OK;
     default:
         return fail(SDDC_ERR_ARG, "unknown parameter %d", param);

@@ -15,12 +15,6 @@ int sddc_ddc_internal_set_variant(sddc_ddc_t *h, int variant);
  * SDDC_DDC_PARAM_FS_STATIC_PCT = the d = 0 kernel's share of each workgroup's frames taken
  * statically before it draws from the dynamic queue (0..100, default kFsStaticPct). */
 #define SDDC_DDC_PARAM_FS_STATIC_PCT 1
-/* SDDC_DDC_PARAM_P_STATIC_PCT = the same for the persistent kernel (d = 1..6 and the d = 0
- * tune bins that are not multiples of 4), every d (default kPStaticPct[d]). */
-#define SDDC_DDC_PARAM_P_STATIC_PCT 2
-/* SDDC_DDC_PARAM_P_TAILWAVE = 1: at d >= 3 the five-wave tail-wave kernel, 0: the four-wave
- * persistent kernel (default kPTailwave). */
-#define SDDC_DDC_PARAM_P_TAILWAVE 3
 int sddc_ddc_internal_set_param(sddc_ddc_t *h, int param, int value);
 /* Diagnostic stamp buffers of -DSDDC_STAMPS builds (tools/fs_stamps.py); -1 in product builds. */
 int sddc_ddc_internal_fs_stamps(unsigned *host, int nwords, int *words_per_wave);

@@ -32,8 +32,8 @@ def shard_pre(nframes, grid, s, per):
     return min(cnt, per * shard_nwg(grid, s))
 
 
-def kstat_of(nframes, grid, pct):   # frame_schedule_kstat
-    return max(1, nframes * pct // (100 * grid))
+def kstat_of(nframes, grid, pct, lo=1):   # frame_schedule_kstat
+    return max(lo, nframes * pct // (100 * grid))
 
 
 class Counters:
@@ -48,18 +48,28 @@ class Counters:
         return old
 
 
-def workgroup(w, nframes, grid, kstat, LA, ctr, out):
+def shard_pairs(cnt, grid, s, ts):   # fs_shard_pairs
+    n = ts * shard_nwg(grid, s)
+    return (cnt - n) >> 1 if cnt > n else 0
+
+
+def workgroup(w, nframes, grid, kstat, LA, ctr, out, ts=4096):
     """one workgroup's frame sequence; yields before each atomic"""
     s_home = w & (SHARDS - 1)
-    q = {"shn": 0, "lo": 0, "cnt": 0, "tk": None, "pv": None}
+    q = {"shn": 0, "lo": 0, "np": 0, "ntk": 0, "tk": None, "pv": None}
+
+    def dyn(s):
+        first = shard_lo(nframes, s) + shard_pre(nframes, grid, s, kstat)
+        return first, shard_lo(nframes, s + 1) - first
 
     def set_shard(sh):
         q["shn"] = sh
         s = (s_home + sh) & (SHARDS - 1)
-        lo = shard_lo(nframes, s)
-        cnt = shard_lo(nframes, s + 1) - lo if sh < SHARDS else 0
-        pre = shard_pre(nframes, grid, s, kstat)
-        q["lo"], q["cnt"] = lo + pre, cnt - pre
+        q["lo"], cnt = dyn(s)
+        if sh >= SHARDS:
+            cnt = 0
+        q["np"] = shard_pairs(cnt, grid, s, ts)
+        q["ntk"] = cnt - q["np"]
 
     def take():
         if q["shn"] < SHARDS:
@@ -71,14 +81,14 @@ def workgroup(w, nframes, grid, kstat, LA, ctr, out):
     def peek():
         q["pv"] = q["tk"]
 
-    def resolve():
-        dry = q["pv"] >= q["cnt"]
+    def resolve():   # -> (frame, second)
+        dry = q["pv"] >= q["ntk"]
         while dry and q["shn"] < SHARDS:
             yield   # the scan: lanes 0..7 add 0 to one counter each (one device-scope atomic)
             live = 0
             for l in range(SHARDS):
-                left = shard_lo(nframes, l + 1) - shard_lo(nframes, l) - shard_pre(nframes, grid, l, kstat)
-                if ctr.c[l] < left:
+                _, cnt = dyn(l)
+                if ctr.c[l] < cnt - shard_pairs(cnt, grid, l, ts):
                     live |= 1 << l
             rot = ((live >> s_home) | (live << (SHARDS - s_home))) & 0xFF
             set_shard((rot & -rot).bit_length() - 1 if rot else SHARDS)
@@ -86,44 +96,54 @@ def workgroup(w, nframes, grid, kstat, LA, ctr, out):
                 break
             yield from take()
             q["pv"] = q["tk"]
-            dry = q["pv"] >= q["cnt"]
-        return -1 if dry else q["lo"] + q["pv"]
+            dry = q["pv"] >= q["ntk"]
+        if dry:
+            return -1, -1
+        pv, lo, np_ = q["pv"], q["lo"], q["np"]
+        return (lo + 2 * pv, lo + 2 * pv + 1) if pv < np_ else (lo + np_ + pv, -1)
 
     nwg = shard_nwg(grid, s_home)
     slo = shard_lo(nframes, s_home) + w // SHARDS
     pre = shard_pre(nframes, grid, s_home, kstat)
     kw = (pre - w // SHARDS + nwg - 1) // nwg if pre > w // SHARDS else 0
     set_shard(0)
+    pend = -1
     known = []
     for i in range(LA):   # first(i)
-        if i < kw:
+        if pend >= 0:
+            known.append(pend)
+            pend = -1
+        elif i < kw:
             known.append(slo + i * nwg)
         else:
             yield from take()
             peek()
-            known.append((yield from resolve()))
-    if LA >= kw:
+            f, pend = yield from resolve()
+            known.append(f)
+    if LA >= kw and pend < 0:
         yield from take()
     j = 0
     while known[0] >= 0:
         out.append(known[0])
-        if j + LA >= kw:   # peek()
+        if j + LA >= kw and pend < 0:   # peek()
             peek()
-        if j + LA < kw:    # next()
+        if pend >= 0:                   # next()
+            fn, pend = pend, -1
+        elif j + LA < kw:
             fn = slo + (j + LA) * nwg
         else:
-            fn = yield from resolve()
-        if j + LA + 1 >= kw:
+            fn, pend = yield from resolve()
+        if pend < 0 and j + LA + 1 >= kw:
             yield from take()
         j += 1
         known = known[1:] + [fn]
 
 
-def run(nframes, grid, pct, LA, seed):
+def run(nframes, grid, pct, LA, seed, ts=4096):
     ctr = Counters()
     out = []
-    kstat = kstat_of(nframes, grid, pct)
-    gens = [workgroup(w, nframes, grid, kstat, LA, ctr, out) for w in range(grid)]
+    kstat = kstat_of(nframes, grid, pct, LA)
+    gens = [workgroup(w, nframes, grid, kstat, LA, ctr, out, ts) for w in range(grid)]
     rng = random.Random(seed)
     live = list(range(grid))
     while live:
@@ -132,7 +152,7 @@ def run(nframes, grid, pct, LA, seed):
             next(gens[i])
         except StopIteration:
             live.remove(i)
-    return out
+    return out, ctr
 
 
 GEOMETRIES = [
@@ -143,12 +163,21 @@ GEOMETRIES = [
 
 
 @pytest.mark.parametrize("nframes,grid", GEOMETRIES)
-@pytest.mark.parametrize("pct", [0, 60, 75, 100])
+@pytest.mark.parametrize("pct", [0, 75, 100])
 @pytest.mark.parametrize("LA", [1, 2])
-def test_every_frame_exactly_once(nframes, grid, pct, LA):
-    for seed in range(3):
-        out = run(nframes, grid, pct, LA, seed)
-        assert sorted(out) == list(range(nframes)), (nframes, grid, pct, LA, seed)
+@pytest.mark.parametrize("ts", [0, 1, 2, 4096])
+def test_every_frame_exactly_once(nframes, grid, pct, LA, ts):
+    for seed in range(2):
+        out, _ = run(nframes, grid, pct, LA, seed, ts)
+        assert sorted(out) == list(range(nframes)), (nframes, grid, pct, LA, seed, ts)
+
+
+def test_pair_tickets_halve_the_dequeues():
+    """headline size, first frames static: tail singles 2 take ~half the tickets of all-singles"""
+    nframes, grid = 11 * 2048, 1024
+    _, c1 = run(nframes, grid, 0, 1, 7, ts=4096)
+    _, c2 = run(nframes, grid, 0, 1, 7, ts=2)
+    assert sum(c2.c) < 0.62 * sum(c1.c), (sum(c1.c), sum(c2.c))
 
 
 def test_static_share_takes_few_tickets():

@@ -64,7 +64,7 @@ def run(lib: str, kernel: str, d: int, nblk: int, tb: int, params=()):
     assert L.sddc_ddc_create(1.0, 0, ctypes.byref(h)) == 0
     L.sddc_ddc_set_tunebin(h, tb)
     L.sddc_ddc_set_decimation(h, d)
-    for k, v in params:   # sddc_ddc_internal_set_param (e.g. 3=0: the four-wave kernel at d >= 3)
+    for k, v in params:   # sddc_ddc_internal_set_param (e.g. 1=40: the d = 0 static share)
         L.sddc_ddc_internal_set_param.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
         assert L.sddc_ddc_internal_set_param(h, k, v) == 0
     dev = torch.device("cuda", 0)
