@@ -155,7 +155,7 @@ __device__ __forceinline__ void tail_pass(float2 *sb, const float2 *twq, int t, 
 }
 
 template <int D, bool RAND, bool NCO, bool CS16>
-__global__ __launch_bounds__(NT, 4) void r2iq_persistent_kernel(
+__global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
     const int *__restrict__ in32, void *__restrict__ out, int nframes,
     const float2 *__restrict__ tw_p1, const float2 *__restrict__ tw_q1,
     const float2 *__restrict__ rec_f, const float2 *__restrict__ rec_i, const float2 *__restrict__ tw4096,

@@ -124,11 +124,12 @@ struct FsQueue {
     // stalled the queue wave ~500 cycles per frame at inverse pass 0, stamps_q15.txt)
     __device__ __forceinline__ void peek() { pv = __builtin_amdgcn_readfirstlane(tk); }
     // the frame of the peeked ticket (second: the pair's second frame, or -1), -1 when every shard
-    // is dry.  A ticket past its shard's end
-    // (this happens only as the queue runs out) scans all eight counters at once (lanes 0..7 add
-    // 0 to one counter each: one device-scope round trip) and moves to the first shard in walk
-    // order from home that still has frames, where it takes (and waits for) a new ticket; with
-    // none left it returns at once.  Walking the shards one atomic at a time instead cost every
+    // is dry.  A ticket past its shard's end (this happens only as the queue runs out) scans all
+    // eight counters at once (lanes 0..7 add 0 to one counter each and compare it with that
+    // shard's ticket count: one device-scope round trip, vector temporaries only; the same test
+    // as a scalar loop over the shards spilled 6 more SGPRs at d = 2) and moves to the first
+    // shard in walk order from home that still has frames, where it takes (and waits for) a new
+    // ticket; with none left it returns at once.  Walking the shards one atomic at a time instead cost every
     // workgroup's last frame 7 serial round trips (~1.2 us each while the chip streams,
     // MI355X_MICROARCH.md dequeue row) on the launch's critical tail.  The counters only grow
     // (until the last workgroup has left), so a shard seen dry stays dry, and a ticket below its
@@ -146,14 +147,11 @@ struct FsQueue {
             const int l = (int)(threadIdx.x & 63);
             const unsigned voff = l < FS_SHARDS ? 64u * (unsigned)l : FS_OOB;
             const int seen = __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(0, rq, voff, 0, 0);
-            unsigned rot = 0;   // bit k: shard home + k has tickets left (scalar: one VGPR in flight)
-#pragma unroll
-            for (int k = 0; k < FS_SHARDS; k++) {
-                const int s = (sh0 + k) & (FS_SHARDS - 1);
-                int first;
-                const int cnt = dyn(s, first);
-                if (__builtin_amdgcn_readlane(seen, s) < cnt - fs_shard_pairs<TS>(cnt, grid, s)) rot |= 1u << k;
-            }
+            int first;
+            const int cnt = dyn(l & (FS_SHARDS - 1), first);
+            const unsigned live = (unsigned)__builtin_amdgcn_ballot_w64(
+                                      l < FS_SHARDS && seen < cnt - fs_shard_pairs<TS>(cnt, grid, l)) & 0xffu;
+            const unsigned rot = ((live >> sh0) | (live << (FS_SHARDS - sh0))) & 0xffu;   // bit k: shard home + k
             set_shard(rot ? __builtin_ctz(rot) : FS_SHARDS);
             if (!rot) break;
             take();
