@@ -480,9 +480,10 @@ def main() -> None:
     ap.add_argument("--tunebin", type=int, default=1024)
     ap.add_argument("--nblk", type=int, default=2048, help="blocks of 65536 per step per GPU")
     ap.add_argument("--mode", choices=["single", "channels"], default="single")
-    ap.add_argument("--streams", type=int, default=1,
+    ap.add_argument("--streams", type=int, default=2,
                     help="single mode: consecutive batches alternate over this many HIP streams (each with its "
-                         "own output buffer), so one batch's launch tail overlaps the next batch's start")
+                         "own output buffer), so one batch's launch tail overlaps the next batch's start "
+                         "(DESIGN.md §5); the roofline comes from a separate single-stream run of the same steps")
     ap.add_argument("--channels", type=int, default=1024)
     ap.add_argument("--bcast", choices=["sag", "bcast"], default="sag",
                     help="C5 input broadcast for N > 1: scatter + all-gather over all links (sag) or one "
@@ -632,6 +633,36 @@ def main() -> None:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall, kern_ms = t.tolist()
 
+    # pipelined batches: the kernel's own launch duration (roofline, rocprof) from the same steps
+    # launched back to back on one stream, timed the same way (max over ranks)
+    single = None
+    if nstreams > 1:
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t1 = time.perf_counter()
+        e0.record(stream)
+        for _ in range(args.steps):
+            ddc.process_device(d_in, nblk, d_out, stream)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        tt = torch.tensor([time.perf_counter() - t1, e0.elapsed_time(e1) / args.steps], dtype=torch.float64,
+                          device=dev if backend == "nccl" else "cpu")
+        if world > 1:
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        wall1, kern1 = tt.tolist()
+        single = {"streams": nstreams, "ms_per_step_single_stream": wall1 * 1e3 / args.steps,
+                  "value_single_stream": samples_per_step_all * args.steps / wall1 / 1e6,
+                  "kernel_ms_single_stream": kern1,
+                  "note": "value: consecutive batches alternate over the streams (each its own output buffer), "
+                          "so one launch's tail overlaps the next one's start; roofline: the kernel's own "
+                          "launch duration, from the same steps on one stream"}
+        kern_ms = kern1
+
     # N > 1 channels: the collective and the compute, each timed alone (max over ranks), so the
     # line shows which of the two bounds the pipelined step
     bcast_info = None
@@ -699,6 +730,8 @@ def main() -> None:
                      "compute": compute_roofline(workload, kern_ms)},
     }
 
+    if single:
+        result["pipelining"] = single
     if bcast_info:
         result["broadcast"] = bcast_info
     if args.mode == "channels" and world > 1:

@@ -265,6 +265,16 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
         }
     }
 
+    // the queue wave takes the ticket for the frame after the next one once this frame's last
+    // loads (the split's P, Q) have been consumed: vmcnt counts in issue order, so a ticket taken
+    // in front of them made the split's wait include the device-scope atomic's round trip (~700
+    // cycles of the queue wave per frame that the other waves waited for at barrier 6, d = 4
+    // stamps, profiles/r04/stamps); it is read at the next frame's top
+    const auto TAKE_NEXT = [&]() {
+        if constexpr (PQ)
+            if (qw) q.take();
+    };
+
     // per-thread constants, live for the whole frame loop
     const int zr = ZROT ? (tunebin >> 8) + (tid < zd ? 1 : 0) : r0;
     const float2 fw1_ = tw4096[(tid + 256 * zr) & (HALF - 1)];   // rotated bases (PRUNE: r0, ZROT: zr)
@@ -333,6 +343,17 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
                 } else {
                     a[r] = make_float2((float)(int)(short)(x[r] & 0xffff), (float)(x[r] >> 16));
                 }
+            // the queue wave reads the ticket taken in the previous frame's middle here, before
+            // this frame's prefetch is issued: its wait then covers only older loads, which have
+            // landed (x was just consumed).  Read after the prefetch (in the middle of the frame,
+            // where it is used), the wait took in the prefetch's HBM latency: ~2000 cycles of
+            // the queue wave per frame that every wave waited for at barrier 5 (d = 3, 4 stamps,
+            // profiles/r04/stamps).  The memory clobber keeps the prefetch below the read.
+            if constexpr (PQ)
+                if (qw) {
+                    q.peek();
+                    asm volatile("" ::"s"(q.pv) : "memory");
+                }
             if (fn >= 0) {   // prefetch the next frame
                 blk = fn / FRAMES;
                 k = fn - blk * FRAMES;
@@ -384,10 +405,8 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
         }
         if (qw) {   // the frame after the next one (read by every wave at the next frame's start)
             if constexpr (PQ) {
-                q.peek();
                 const int g = q.resolve();
                 if (tid == QLANE) s_next = g;
-                q.take();
             } else if (tid == QLANE) {
                 s_next = fn >= 0 && fn + 1 < f1s ? fn + 1 : -1;
             }
@@ -427,6 +446,7 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
                         float2 u0[R0];
                         if constexpr (R0 == 8) dft8<+1>(a, u0);   // pass 0 (Ns = 1)
                         else dft4<+1>(a, u0);
+                        TAKE_NEXT();
                         ST_SYNC(6);   // every wave's Z reads are done
 #pragma unroll
                         for (int r = 0; r < R0; r++) w1[wg_swz<N>(R0 * t + r)] = u0[r];
@@ -461,6 +481,7 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
                     // d = 3: the 512 filtered bins (inverse input m = t + 256 r) go to LDS, and wave 0
                     // runs the inverse as three radix-8 Stockham passes (tail_pass) instead of the
                     // radix-2 pass on every thread and two radix-16 passes on 32 lanes
+                    TAKE_NEXT();
                     ST_SYNC(6);   // every wave's Z reads are done
 #pragma unroll
                     for (int r = 0; r < R0; r++) w1[tail_swz<N>(t + NT * r)] = a[r];
@@ -480,6 +501,7 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
                 if constexpr (R0 == 16) dft16<+1>(a, u);
                 else dft<R0, +1>(a, u);
             }
+            TAKE_NEXT();
             ST_SYNC(6);
             if constexpr (R0 == 16) {
 #pragma unroll
@@ -547,6 +569,7 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
             }
             // the N filtered bins to sb, then wave 0 runs the inverse as Stockham passes
             if (t < N) sb[tail_swz<N>(t)] = tv;
+            TAKE_NEXT();
             ST_SYNC(6);
             if (t < 64) {
                 float2 u[8];

@@ -1,0 +1,8 @@
+# round 4, session i: the ticket taken after the split's loads (persistent kernel), queue at d >= 3
+set -o pipefail
+O=gpurun_out/r04_i; mkdir -p $O
+timeout -k 10 500 python -u tools/ab_libs.py --libs build/ab/base.so build/ab/cur3.so build/ab/cur4.so build/ab/pqall3.so --d 1 2 3 4 5 6 --rounds 5 > $O/ab.log 2>&1 || exit $?
+for d in 1 4; do
+timeout -k 10 120 python -u tools/fs_stamps.py --kernel p --d $d --libs build/ab/pqst3.so > $O/stamps_pq3_d$d.log 2>&1 || exit $?
+done
+echo done > $O/DONE
