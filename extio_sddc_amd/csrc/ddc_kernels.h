@@ -73,7 +73,15 @@ struct KernelTables {
 hipError_t launch_frames_persistent(const KernelTables &t, int d, const int16_t *d_in, int nblk,
                                     void *d_out, const float4 *pq, int tunebin, int lsb, int rand,
                                     int cs16, float cs16_scale, const float2 *nco_starts,
-                                    const float2 *nco_trig, unsigned *wq, int device, hipStream_t s);
+                                    const float2 *nco_trig, unsigned *wq, int slot_weights, int device,
+                                    hipStream_t s);
+// slot_weights (d >= 3): split the frames over the workgroups by their CU slot's measured speed
+// (kSlotWeights[d]: slot 0 in the low byte; ddc_queue.hpp slot_split), 0: equal contiguous ranges
+constexpr unsigned slot_weights4(unsigned a, unsigned b, unsigned c, unsigned e) { return a | (b << 8) | (c << 16) | (e << 24); }
+constexpr unsigned kSlotWeights[7] = {0u, slot_weights4(29, 25, 19, 15), slot_weights4(29, 25, 19, 15),
+                                      slot_weights4(27, 24, 20, 16), slot_weights4(27, 24, 20, 16),
+                                      slot_weights4(27, 24, 20, 16), slot_weights4(27, 24, 20, 16)};
+constexpr int kSlotWeighting = 1;
 hipError_t launch_build_split_filter(const KernelTables &t, int d, int tunebin, float4 *pq, hipStream_t s);
 
 // d = 0 fused-split kernel (ddc_fs.hip, FS): used when fs_path(d, tunebin) (d = 0, tunebin a

@@ -159,7 +159,7 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
     const int *__restrict__ in32, void *__restrict__ out, int nframes,
     const float2 *__restrict__ tw_p1, const float2 *__restrict__ tw_q1,
     const float2 *__restrict__ rec_f, const float2 *__restrict__ rec_i, const float2 *__restrict__ tw4096,
-    const float4 *__restrict__ pq, int tunebin, OutArgs oa, NcoArgs nco, unsigned *__restrict__ wq)
+    const float4 *__restrict__ pq, int tunebin, OutArgs oa, NcoArgs nco, unsigned *__restrict__ wq, unsigned slotw)
 {
     constexpr int N = HALF >> D;
     // d >= 2 (N <= 1024): the inverse reads only the band [s0, s0 + N) of Z and its mirror
@@ -235,7 +235,7 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
     __shared__ int s_first, s_next;
     constexpr int QLANE = 64 * 3;
     const bool qw = __builtin_amdgcn_readfirstlane(tid >> 6) == 3;
-    const int f1s = (int)(((long long)nframes * (w + 1)) / G);   // the static split's range end
+    const int f1s = PQ ? 0 : slot_split(nframes, G, w + 1, slotw);   // the static split's range end
     FsQueue<-1> q;   // (the FrameSchedule's extra scalar state spilled 19-27 SGPRs at d = 2)
     if constexpr (PQ) q.init(wq, nframes, w & (FS_SHARDS - 1), G, 2);
     if (qw) {
@@ -255,7 +255,7 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
             }
             q.take();
         } else {
-            const int f0 = (int)(((long long)nframes * w) / G);
+            const int f0 = slot_split(nframes, G, w, slotw);
             g[0] = f0 < f1s ? f0 : -1;
             g[1] = f0 + 1 < f1s ? f0 + 1 : -1;
         }
@@ -270,8 +270,12 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
     // in front of them made the split's wait include the device-scope atomic's round trip (~700
     // cycles of the queue wave per frame that the other waves waited for at barrier 6, d = 4
     // stamps, profiles/r04/stamps); it is read at the next frame's top
+    // (d = 0, the persistent kernel's tune bins that are not multiples of 4: taken in the middle of
+    // the frame, as before; taken late, the atomic's result register raised the kernel to 128
+    // VGPRs with 61 spilled)
+    constexpr bool LATE_TAKE = D >= 1;
     const auto TAKE_NEXT = [&]() {
-        if constexpr (PQ)
+        if constexpr (PQ && LATE_TAKE)
             if (qw) q.take();
     };
 
@@ -407,6 +411,7 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
             if constexpr (PQ) {
                 const int g = q.resolve();
                 if (tid == QLANE) s_next = g;
+                if constexpr (!LATE_TAKE) q.take();
             } else if (tid == QLANE) {
                 s_next = fn >= 0 && fn + 1 < f1s ? fn + 1 : -1;
             }
@@ -624,6 +629,7 @@ struct Launch {
     OutArgs oa;
     NcoArgs nco;
     unsigned *wq;   // a zeroed dynamic-frame-queue slot (kFsQueueWords)
+    unsigned slotw; // d >= 3: the static split's slot weights (ddc_queue.hpp slot_split), 0: equal
 };
 
 template <int D, bool RAND, bool NCO, bool CS16>
@@ -638,7 +644,7 @@ hipError_t launch_v(const KernelTables &t, const Launch &L)
     if (grid > nframes) grid = nframes;
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), 0, L.s, reinterpret_cast<const int *>(L.d_in),
                        L.d_out, nframes, t.tw_p1, t.tw_q1[D], t.rec_f, t.rec_i[D], t.tw4096, L.pq, L.tunebin, L.oa,
-                       L.nco, L.wq);
+                       L.nco, L.wq, occ == 4 && grid == cus * occ ? L.slotw : 0u);
     return hipGetLastError();
 }
 
@@ -669,11 +675,11 @@ hipError_t launch_build_split_filter(const KernelTables &t, int d, int tunebin, 
 
 hipError_t launch_frames_persistent(const KernelTables &t, int d, const int16_t *d_in, int nblk, void *d_out,
                                     const float4 *pq, int tunebin, int lsb, int rand, int cs16, float cs16_scale,
-                                    const float2 *nco_starts, const float2 *nco_trig, unsigned *wq, int device,
-                                    hipStream_t s)
+                                    const float2 *nco_starts, const float2 *nco_trig, unsigned *wq, int slot_weights,
+                                    int device, hipStream_t s)
 {
     const Launch L{d_in, nblk, d_out, pq, tunebin, device, s, OutArgs{lsb ? 0x80000000u : 0u, cs16_scale},
-                   NcoArgs{nco_starts, nco_trig}, wq};
+                   NcoArgs{nco_starts, nco_trig}, wq, slot_weights && d >= 1 && d <= 6 ? kSlotWeights[d] : 0u};
     const bool f = cs16 != 0;
     switch (d) {
     case 0: return launch_d<0>(t, L, rand, f);

@@ -242,6 +242,28 @@ struct FrameSchedule {
     }
 };
 
+// Slot-weighted static split.  A full-residency launch (grid = 4 x CUs) places blockIdx quarter q
+// on CU slot q (HW_ID TG_ID, all 1024 workgroups, stamps in profiles/r04/stamps), and a CU's
+// SIMDs arbitrate by age, so slot q runs at a fixed fraction of slot 0's speed (d = 4: 1, 0.89,
+// 0.74, 0.59 frames per us while all four are resident).  An equal contiguous split left slot 0
+// done at 75 us and slot 3 at 113 us of a 124 us launch; weighted shares end them together.
+// slotw: four 8-bit weights (slot 0 in the low byte), 0: equal shares.  First frame of workgroup
+// v (v = G: nframes).
+__device__ __forceinline__ int slot_split(int nframes, int G, int v, unsigned slotw)
+{
+    if (slotw == 0u || (G & 3)) return (int)(((long long)nframes * v) / G);
+    const int Q = G >> 2, q = v / Q, i = v - q * Q;
+    long long sw = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int wk = (int)((slotw >> (8 * k)) & 0xffu);
+        tot += (long long)Q * wk;
+        if (k < q) sw += (long long)Q * wk;
+        else if (k == q) sw += (long long)i * wk;
+    }
+    return (int)(((long long)nframes * sw) / tot);
+}
+
 // static frames per workgroup for a static share of pct percent, at least lo (the schedule's
 // lookahead: the frames a workgroup needs before its first ticket could have returned)
 inline int frame_schedule_kstat(int nframes, int grid, int pct, int lo)

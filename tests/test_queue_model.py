@@ -213,3 +213,35 @@ def test_last_frame_needs_one_scan():
     steps = sum(1 for _ in g)
     assert out == [shard_lo(nframes, 0)]   # its static frame only
     assert steps <= 3   # the ticket taken ahead, one scan, (no more)
+
+
+def slot_split(nframes, G, v, slotw):   # ddc_queue.hpp slot_split
+    if slotw == 0 or G & 3:
+        return nframes * v // G
+    Q = G >> 2
+    q, i = v // Q, v - (v // Q) * Q
+    sw = tot = 0
+    for k in range(4):
+        wk = (slotw >> (8 * k)) & 0xFF
+        tot += Q * wk
+        if k < q:
+            sw += Q * wk
+        elif k == q:
+            sw += i * wk
+    return nframes * sw // tot
+
+
+@pytest.mark.parametrize("nframes,G", [(11 * 2048, 1024), (11 * 256, 1024), (11 * 93, 1020), (11 * 64, 704), (4, 4), (11, 11)])
+@pytest.mark.parametrize("slotw", [0, 27 | 24 << 8 | 20 << 16 | 16 << 24, 29 | 25 << 8 | 19 << 16 | 15 << 24])
+def test_slot_split_partitions_the_frames(nframes, G, slotw):
+    """the slot-weighted static split (d >= 3): contiguous ranges that cover every frame once, in
+    the slots' proportions"""
+    starts = [slot_split(nframes, G, v, slotw) for v in range(G + 1)]
+    assert starts[0] == 0 and starts[-1] == nframes
+    assert all(a <= b for a, b in zip(starts, starts[1:]))
+    if slotw and G % 4 == 0 and nframes >= 4 * G:
+        Q = G // 4
+        per = [starts[(q + 1) * Q] - starts[q * Q] for q in range(4)]
+        w = [(slotw >> (8 * k)) & 0xFF for k in range(4)]
+        for q in range(4):
+            assert abs(per[q] / nframes - w[q] / sum(w)) < 1e-3

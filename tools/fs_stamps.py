@@ -124,6 +124,13 @@ def main():
               f"end: min {re_us.min():.1f} p10 {np.percentile(re_us, 10):.1f} p50 {np.median(re_us):.1f} "
               f"p90 {np.percentile(re_us, 90):.1f} max {re_us.max():.1f}")
         print(f"  frames per workgroup: min {fr[:, 0].min():.0f} p50 {np.median(fr[:, 0]):.0f} max {fr[:, 0].max():.0f}")
+        hw = st[:, 0, 2 * SEGS + 6].astype(np.int64)
+        tg = (hw >> 16) & 0xF   # HW_ID TG_ID (bits 19:16): the workgroup slot on its CU
+        for q in range(4):
+            sel = (np.arange(len(re_us)) * 4 // len(re_us)) == q
+            print(f"    blockIdx quarter {q}: end p50 {np.median(re_us[sel]):.1f} us, frames p50 {np.median(fr[sel, 0]):.0f}"
+                  f"; HW slot {q}: {int(np.sum(tg == q))} workgroups, end p50 "
+                  f"{np.median(re_us[tg == q]) if np.any(tg == q) else float('nan'):.1f} us")
         lo = 4 * (which - 1)
         rows = []
         for i in range(SEGS):
