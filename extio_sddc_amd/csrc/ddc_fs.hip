@@ -121,7 +121,7 @@ template <bool RAND, bool LSB, bool NCO, bool CS16>
 __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
     const int *__restrict__ in32, void *__restrict__ out, int nframes, const float2 *__restrict__ tw_p1,
     const float2 *__restrict__ rec_f, const float4 *__restrict__ pqf, const float2 *__restrict__ fsl, int tunebin,
-    OutArgs oa, NcoArgs nco, unsigned *__restrict__ wq, int kstat)
+    OutArgs oa, NcoArgs nco, unsigned *__restrict__ wq, int ns, unsigned slotw)
 {
     __shared__ __attribute__((aligned(16))) float2 lds[kFsLds];
     // F1 twiddles W_256^{s r} [15][16] (I1 conjugates them: at d = 0 its table is the same) and
@@ -143,11 +143,12 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
     {
         // every wave knows the first frame (it is static unless the batch is small): its input
         // loads go out at once, ahead of the table copies
-        const int f0s = fs_static_frame(nframes, (int)gridDim.x, w, 0, kstat);
+        const int G = (int)gridDim.x, a0 = slot_split(ns, G, w, slotw);
+        const int f0s = a0 < slot_split(ns, G, w + 1, slotw) ? a0 : -1;
         if (f0s >= 0) load_frame(in32, f0s / FRAMES, f0s % FRAMES, x);
         if (qw) {
             int f0[1];
-            fsch.init(wq, nframes, w, (int)gridDim.x, kstat, f0);
+            fsch.init(wq, nframes, ns, w, G, slotw, f0);
             if (tid == QLANE) s_next = f0[0];
         }
         for (int i = tid; i < 15 * 16; i += NT) twl[i] = tw_p1[i];
@@ -283,8 +284,7 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
 #pragma unroll
             for (int r = 0; r < 16; r++) st_row(lds, xc0, r, 0, u[r]);
         }
-        // the next frame (static, or the ticket read at this frame's top), then a ticket for the
-        // one after it when that one is dynamic (ddc_queue.hpp)
+        // the next frame (static, or the ticket read at this frame's top; ddc_queue.hpp)
         if (qw) {
             const int f_n = fsch.next();
             if (tid == QLANE) s_next = f_n;
@@ -314,6 +314,10 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
                 k = fn - blk * FRAMES;
                 load_frame(in32, blk, k, x);
             }
+            // the ticket for the frame after the next one, when that one is dynamic: behind this
+            // frame's last loads (vmcnt counts in issue order: taken at inverse pass 0, the wait
+            // for I2's lane factors included the atomic); read at the next frame's top
+            if (qw) fsch.take();
             table_twiddle<+1, true>(a, twl, 16, x15);
             dft16<+1>(a, u);
         }
@@ -395,9 +399,10 @@ hipError_t launch_fs_v(const KernelTables &t, const int16_t *d_in, int nblk, voi
     const int nframes = nblk * FRAMES;
     int grid = cus * occ;
     if (grid > nframes) grid = nframes;
-    const int kstat = frame_schedule_kstat(nframes, grid, static_pct, 1);
+    const int ns = frame_schedule_static(nframes, static_pct);
+    const unsigned slotw = occ == 4 && grid == cus * occ ? kFsSlotWeights : 0u;
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), 0, s, reinterpret_cast<const int *>(d_in), d_out, nframes,
-                       t.tw_p1, t.rec_f, pqf, fsl, tunebin, oa, nco, wq, kstat);
+                       t.tw_p1, t.rec_f, pqf, fsl, tunebin, oa, nco, wq, ns, slotw);
     return hipGetLastError();
 }
 

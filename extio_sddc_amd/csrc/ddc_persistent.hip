@@ -159,7 +159,8 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
     const int *__restrict__ in32, void *__restrict__ out, int nframes,
     const float2 *__restrict__ tw_p1, const float2 *__restrict__ tw_q1,
     const float2 *__restrict__ rec_f, const float2 *__restrict__ rec_i, const float2 *__restrict__ tw4096,
-    const float4 *__restrict__ pq, int tunebin, OutArgs oa, NcoArgs nco, unsigned *__restrict__ wq, unsigned slotw)
+    const float4 *__restrict__ pq, int tunebin, OutArgs oa, NcoArgs nco, unsigned *__restrict__ wq, int ns,
+    unsigned slotw)
 {
     constexpr int N = HALF >> D;
     // d >= 2 (N <= 1024): the inverse reads only the band [s0, s0 + N) of Z and its mirror
@@ -223,37 +224,23 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
 
     const int tid = (int)threadIdx.x;
     const int G = (int)gridDim.x, w = (int)blockIdx.x;
-    // d <= 2: frames come from the dynamic frame queue (ddc_queue.hpp), worked by wave 3, after
-    // two static frames per workgroup (fs_static_frame: no atomic round trip before the first
-    // frames): the frame after the next one is learnt in the middle of each frame (the next one's
-    // input is prefetched at the frame's start), from a ticket taken a frame earlier.  d = 1 +4 %, d = 2 +1 % against a
-    // static split, but d = 3 -2 % and d = 4 -4 % (their frames are short and the queue wave's
-    // bookkeeping is not), so d >= 3 keep the static contiguous split (profiles/r03/ab/
-    // pq_dynamic_queue_d1_4.txt, p_queue_d3_6_after_tails.txt; round 4 re-measured a static prefix
-    // of 75 % at every d: d = 3, 4 -4 %, d = 1, 2 -1 to -2 %, profiles/r04/ab).
+    // Frames: d <= 2 the frame schedule (ddc_queue.hpp FrameSchedule: a slot-weighted static split
+    // of the first ns frames, then the dynamic queue), worked by wave 3: the frame after the next
+    // one is learnt in the middle of each frame (the next one's input is prefetched at the frame's
+    // start), from a ticket read at the frame's top.  d >= 3: the slot-weighted static split of
+    // every frame, no queue (the queue's per-frame cost, ~2k cycles of a ~10k-cycle frame at d = 4
+    // in round 4's stamps, is more than the imbalance it removes once the split is weighted;
+    // profiles/r04/stamps, profiles/r04/ab).
     constexpr bool PQ = D <= 2;
     __shared__ int s_first, s_next;
     constexpr int QLANE = 64 * 3;
     const bool qw = __builtin_amdgcn_readfirstlane(tid >> 6) == 3;
     const int f1s = PQ ? 0 : slot_split(nframes, G, w + 1, slotw);   // the static split's range end
-    FsQueue<-1> q;   // (the FrameSchedule's extra scalar state spilled 19-27 SGPRs at d = 2)
-    if constexpr (PQ) q.init(wq, nframes, w & (FS_SHARDS - 1), G, 2);
+    FrameSchedule<2> fsch;
     if (qw) {
         int g[2];
         if constexpr (PQ) {
-            g[0] = fs_static_frame(nframes, G, w, 0, 2);
-            g[1] = fs_static_frame(nframes, G, w, 1, 2);
-            if (g[0] < 0) {   // no static frames (small batches): both from the queue
-                q.take();
-                q.peek();
-                g[0] = q.resolve();
-            }
-            if (g[1] < 0) {
-                q.take();
-                q.peek();
-                g[1] = g[0] >= 0 ? q.resolve() : -1;
-            }
-            q.take();
+            fsch.init(wq, nframes, ns, w, G, slotw, g);
         } else {
             const int f0 = slot_split(nframes, G, w, slotw);
             g[0] = f0 < f1s ? f0 : -1;
@@ -276,7 +263,7 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
     constexpr bool LATE_TAKE = D >= 1;
     const auto TAKE_NEXT = [&]() {
         if constexpr (PQ && LATE_TAKE)
-            if (qw) q.take();
+            if (qw) fsch.take();
     };
 
     // per-thread constants, live for the whole frame loop
@@ -355,8 +342,8 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
             // profiles/r04/stamps).  The memory clobber keeps the prefetch below the read.
             if constexpr (PQ)
                 if (qw) {
-                    q.peek();
-                    asm volatile("" ::"s"(q.pv) : "memory");
+                    fsch.peek();
+                    asm volatile("" ::"s"(fsch.q.pv) : "memory");
                 }
             if (fn >= 0) {   // prefetch the next frame
                 blk = fn / FRAMES;
@@ -409,9 +396,9 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
         }
         if (qw) {   // the frame after the next one (read by every wave at the next frame's start)
             if constexpr (PQ) {
-                const int g = q.resolve();
+                const int g = fsch.next();
                 if (tid == QLANE) s_next = g;
-                if constexpr (!LATE_TAKE) q.take();
+                if constexpr (!LATE_TAKE) fsch.take();
             } else if (tid == QLANE) {
                 s_next = fn >= 0 && fn + 1 < f1s ? fn + 1 : -1;
             }
@@ -629,7 +616,8 @@ struct Launch {
     OutArgs oa;
     NcoArgs nco;
     unsigned *wq;   // a zeroed dynamic-frame-queue slot (kFsQueueWords)
-    unsigned slotw; // d >= 3: the static split's slot weights (ddc_queue.hpp slot_split), 0: equal
+    unsigned slotw; // the static split's slot weights (ddc_queue.hpp slot_split), 0: equal
+    int static_pct; // d <= 2: the statically split share of the frames (the rest: the queue)
 };
 
 template <int D, bool RAND, bool NCO, bool CS16>
@@ -644,7 +632,8 @@ hipError_t launch_v(const KernelTables &t, const Launch &L)
     if (grid > nframes) grid = nframes;
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), 0, L.s, reinterpret_cast<const int *>(L.d_in),
                        L.d_out, nframes, t.tw_p1, t.tw_q1[D], t.rec_f, t.rec_i[D], t.tw4096, L.pq, L.tunebin, L.oa,
-                       L.nco, L.wq, occ == 4 && grid == cus * occ ? L.slotw : 0u);
+                       L.nco, L.wq, frame_schedule_static(nframes, L.static_pct),
+                       occ == 4 && grid == cus * occ ? L.slotw : 0u);
     return hipGetLastError();
 }
 
@@ -676,10 +665,12 @@ hipError_t launch_build_split_filter(const KernelTables &t, int d, int tunebin, 
 hipError_t launch_frames_persistent(const KernelTables &t, int d, const int16_t *d_in, int nblk, void *d_out,
                                     const float4 *pq, int tunebin, int lsb, int rand, int cs16, float cs16_scale,
                                     const float2 *nco_starts, const float2 *nco_trig, unsigned *wq, int slot_weights,
-                                    int device, hipStream_t s)
+                                    int static_pct, int device, hipStream_t s)
 {
+    if (static_pct < 0 || static_pct > 100) return hipErrorInvalidValue;
     const Launch L{d_in, nblk, d_out, pq, tunebin, device, s, OutArgs{lsb ? 0x80000000u : 0u, cs16_scale},
-                   NcoArgs{nco_starts, nco_trig}, wq, slot_weights && d >= 1 && d <= 6 ? kSlotWeights[d] : 0u};
+                   NcoArgs{nco_starts, nco_trig}, wq, slot_weights && d >= 0 && d <= 6 ? kSlotWeights[d] : 0u,
+                   static_pct};
     const bool f = cs16 != 0;
     switch (d) {
     case 0: return launch_d<0>(t, L, rand, f);
