@@ -73,18 +73,17 @@ struct KernelTables {
 hipError_t launch_frames_persistent(const KernelTables &t, int d, const int16_t *d_in, int nblk,
                                     void *d_out, const float4 *pq, int tunebin, int lsb, int rand,
                                     int cs16, float cs16_scale, const float2 *nco_starts,
-                                    const float2 *nco_trig, unsigned *wq, int slot_weights, int static_pct,
-                                    int device, hipStream_t s);
-// slot_weights: split the statically scheduled frames over the workgroups by their CU slot's
-// measured speed (kSlotWeights[d]: slot 0 in the low byte; ddc_queue.hpp slot_split), 0: equal
-// contiguous ranges.  static_pct (d <= 2): the statically split share of the frames, the rest
-// from the dynamic queue (kPStaticPct[d]; d >= 3 split every frame statically).
+                                    const float2 *nco_trig, int slot_weights, int device, hipStream_t s);
+// slot_weights: split the frames over the workgroups by their CU slot's measured speed
+// (kSlotWeights[d]: slot 0 in the low byte; ddc_queue.hpp slot_split), 0: equal contiguous
+// ranges.  The frames per slot of a balanced (queue-fed) run gave the weights: d = 1 29 / 25 /
+// 19 / 15, d = 4 27 / 24 / 20 / 16, tuned at d >= 3 to 29 / 25 / 20 / 15 (+3-6 %,
+// profiles/r04/ab/slot_weights_d3_6.txt).
 constexpr unsigned slot_weights4(unsigned a, unsigned b, unsigned c, unsigned e) { return a | (b << 8) | (c << 16) | (e << 24); }
 constexpr unsigned kSlotWeights[7] = {slot_weights4(29, 25, 19, 15), slot_weights4(29, 25, 19, 15), slot_weights4(29, 25, 19, 15),
-                                      slot_weights4(27, 24, 20, 16), slot_weights4(27, 24, 20, 16),
-                                      slot_weights4(27, 24, 20, 16), slot_weights4(27, 24, 20, 16)};
+                                      slot_weights4(29, 25, 20, 15), slot_weights4(29, 25, 20, 15),
+                                      slot_weights4(29, 25, 20, 15), slot_weights4(29, 25, 20, 15)};
 constexpr int kSlotWeighting = 1;
-constexpr int kPStaticPct[7] = {85, 85, 85, 100, 100, 100, 100};
 hipError_t launch_build_split_filter(const KernelTables &t, int d, int tunebin, float4 *pq, hipStream_t s);
 
 // d = 0 fused-split kernel (ddc_fs.hip, FS): used when fs_path(d, tunebin) (d = 0, tunebin a
@@ -99,7 +98,7 @@ hipError_t launch_build_fs_tables(const KernelTables &t, int tunebin, float4 *pq
 // from the queue (ddc_queue.hpp FrameSchedule); kFsStaticPct by default.
 constexpr int kFsQueueWords = 16 * 9;
 constexpr int kFsStaticPct = 85;
-constexpr unsigned kFsSlotWeights = slot_weights4(29, 25, 19, 15);
+constexpr unsigned kFsSlotWeights = slot_weights4(30, 25, 19, 14);   // (FS frames per slot, queue-fed)
 hipError_t launch_frames_fs(const KernelTables &t, const int16_t *d_in, int nblk, void *d_out, const float4 *pqf,
                             const float2 *fsl, int tunebin, int lsb, int rand, int cs16, float cs16_scale,
                             const float2 *nco_starts, const float2 *nco_trig, unsigned *wq, int static_pct,

@@ -159,8 +159,7 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
     const int *__restrict__ in32, void *__restrict__ out, int nframes,
     const float2 *__restrict__ tw_p1, const float2 *__restrict__ tw_q1,
     const float2 *__restrict__ rec_f, const float2 *__restrict__ rec_i, const float2 *__restrict__ tw4096,
-    const float4 *__restrict__ pq, int tunebin, OutArgs oa, NcoArgs nco, unsigned *__restrict__ wq, int ns,
-    unsigned slotw)
+    const float4 *__restrict__ pq, int tunebin, OutArgs oa, NcoArgs nco, unsigned slotw)
 {
     constexpr int N = HALF >> D;
     // d >= 2 (N <= 1024): the inverse reads only the band [s0, s0 + N) of Z and its mirror
@@ -224,47 +223,25 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
 
     const int tid = (int)threadIdx.x;
     const int G = (int)gridDim.x, w = (int)blockIdx.x;
-    // Frames: d <= 2 the frame schedule (ddc_queue.hpp FrameSchedule: a slot-weighted static split
-    // of the first ns frames, then the dynamic queue), worked by wave 3: the frame after the next
-    // one is learnt in the middle of each frame (the next one's input is prefetched at the frame's
-    // start), from a ticket read at the frame's top.  d >= 3: the slot-weighted static split of
-    // every frame, no queue (the queue's per-frame cost, ~2k cycles of a ~10k-cycle frame at d = 4
-    // in round 4's stamps, is more than the imbalance it removes once the split is weighted;
-    // profiles/r04/stamps, profiles/r04/ab).
-    constexpr bool PQ = D <= 2;
+    // Frames: a static split, each workgroup one contiguous range, sized by its CU slot's measured
+    // speed (ddc_queue.hpp slot_split; equal shares off full residency).  Wave 3 writes the next
+    // frame number for the next frame's start.  Round 3 fed d = 1, 2 from the dynamic frame
+    // queue (two static frames, then one ticket per frame) and split d >= 3 equally; the weighted
+    // split beats both: d = 1 +3 %, d = 2 +6-8 % against the queue, d = 3..6 +10-14 % against the
+    // equal split (profiles/r04/ab/slot_weighted_*.txt).  The queue cost this kernel ~1-2k cycles
+    // of a 10-16k-cycle frame even with its ticket read and taken where no load waits for it
+    // (profiles/r04/stamps/stamps_p_d*_queue_*.txt).
     __shared__ int s_first, s_next;
     constexpr int QLANE = 64 * 3;
     const bool qw = __builtin_amdgcn_readfirstlane(tid >> 6) == 3;
-    const int f1s = PQ ? 0 : slot_split(nframes, G, w + 1, slotw);   // the static split's range end
-    FrameSchedule<2> fsch;
+    const int f1s = slot_split(nframes, G, w + 1, slotw);   // the range's end
     if (qw) {
-        int g[2];
-        if constexpr (PQ) {
-            fsch.init(wq, nframes, ns, w, G, slotw, g);
-        } else {
-            const int f0 = slot_split(nframes, G, w, slotw);
-            g[0] = f0 < f1s ? f0 : -1;
-            g[1] = f0 + 1 < f1s ? f0 + 1 : -1;
-        }
+        const int f0 = slot_split(nframes, G, w, slotw);
         if (tid == QLANE) {
-            s_first = g[0];
-            s_next = g[1];
+            s_first = f0 < f1s ? f0 : -1;
+            s_next = f0 + 1 < f1s ? f0 + 1 : -1;
         }
     }
-
-    // the queue wave takes the ticket for the frame after the next one once this frame's last
-    // loads (the split's P, Q) have been consumed: vmcnt counts in issue order, so a ticket taken
-    // in front of them made the split's wait include the device-scope atomic's round trip (~700
-    // cycles of the queue wave per frame that the other waves waited for at barrier 6, d = 4
-    // stamps, profiles/r04/stamps); it is read at the next frame's top
-    // (d = 0, the persistent kernel's tune bins that are not multiples of 4: taken in the middle of
-    // the frame, as before; taken late, the atomic's result register raised the kernel to 128
-    // VGPRs with 61 spilled)
-    constexpr bool LATE_TAKE = D >= 1;
-    const auto TAKE_NEXT = [&]() {
-        if constexpr (PQ && LATE_TAKE)
-            if (qw) fsch.take();
-    };
 
     // per-thread constants, live for the whole frame loop
     const int zr = ZROT ? (tunebin >> 8) + (tid < zd ? 1 : 0) : r0;
@@ -334,17 +311,6 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
                 } else {
                     a[r] = make_float2((float)(int)(short)(x[r] & 0xffff), (float)(x[r] >> 16));
                 }
-            // the queue wave reads the ticket taken in the previous frame's middle here, before
-            // this frame's prefetch is issued: its wait then covers only older loads, which have
-            // landed (x was just consumed).  Read after the prefetch (in the middle of the frame,
-            // where it is used), the wait took in the prefetch's HBM latency: ~2000 cycles of
-            // the queue wave per frame that every wave waited for at barrier 5 (d = 3, 4 stamps,
-            // profiles/r04/stamps).  The memory clobber keeps the prefetch below the read.
-            if constexpr (PQ)
-                if (qw) {
-                    fsch.peek();
-                    asm volatile("" ::"s"(fsch.q.pv) : "memory");
-                }
             if (fn >= 0) {   // prefetch the next frame
                 blk = fn / FRAMES;
                 k = fn - blk * FRAMES;
@@ -394,15 +360,8 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
 #pragma unroll
             for (int r = 0; r < 16; r++) w0[sZ + NT * r] = v[r];   // Z, rotated by tb
         }
-        if (qw) {   // the frame after the next one (read by every wave at the next frame's start)
-            if constexpr (PQ) {
-                const int g = fsch.next();
-                if (tid == QLANE) s_next = g;
-                if constexpr (!LATE_TAKE) fsch.take();
-            } else if (tid == QLANE) {
-                s_next = fn >= 0 && fn + 1 < f1s ? fn + 1 : -1;
-            }
-        }
+        if (tid == QLANE)   // the frame after the next one (read by every wave at the next frame's start)
+            s_next = fn >= 0 && fn + 1 < f1s ? fn + 1 : -1;
         ST_SYNC(5);
 
         if constexpr (N >= 512) {
@@ -438,8 +397,7 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
                         float2 u0[R0];
                         if constexpr (R0 == 8) dft8<+1>(a, u0);   // pass 0 (Ns = 1)
                         else dft4<+1>(a, u0);
-                        TAKE_NEXT();
-                        ST_SYNC(6);   // every wave's Z reads are done
+                                                ST_SYNC(6);   // every wave's Z reads are done
 #pragma unroll
                         for (int r = 0; r < R0; r++) w1[wg_swz<N>(R0 * t + r)] = u0[r];
                     }
@@ -473,8 +431,7 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
                     // d = 3: the 512 filtered bins (inverse input m = t + 256 r) go to LDS, and wave 0
                     // runs the inverse as three radix-8 Stockham passes (tail_pass) instead of the
                     // radix-2 pass on every thread and two radix-16 passes on 32 lanes
-                    TAKE_NEXT();
-                    ST_SYNC(6);   // every wave's Z reads are done
+                                        ST_SYNC(6);   // every wave's Z reads are done
 #pragma unroll
                     for (int r = 0; r < R0; r++) w1[tail_swz<N>(t + NT * r)] = a[r];
                     ST_SYNC(7);
@@ -493,8 +450,7 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
                 if constexpr (R0 == 16) dft16<+1>(a, u);
                 else dft<R0, +1>(a, u);
             }
-            TAKE_NEXT();
-            ST_SYNC(6);
+                        ST_SYNC(6);
             if constexpr (R0 == 16) {
 #pragma unroll
                 for (int r = 0; r < 16; r++)
@@ -561,8 +517,7 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
             }
             // the N filtered bins to sb, then wave 0 runs the inverse as Stockham passes
             if (t < N) sb[tail_swz<N>(t)] = tv;
-            TAKE_NEXT();
-            ST_SYNC(6);
+                        ST_SYNC(6);
             if (t < 64) {
                 float2 u[8];
                 const float2 *twq = twl + 15 * 16;
@@ -577,8 +532,6 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
         f = fn;
     }
     ST_WRITE(g_p_stamps, w, tid);
-    if constexpr (PQ)
-        if (tid == QLANE) fs_queue_done(wq, (unsigned)G);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -615,9 +568,7 @@ struct Launch {
     hipStream_t s;
     OutArgs oa;
     NcoArgs nco;
-    unsigned *wq;   // a zeroed dynamic-frame-queue slot (kFsQueueWords)
     unsigned slotw; // the static split's slot weights (ddc_queue.hpp slot_split), 0: equal
-    int static_pct; // d <= 2: the statically split share of the frames (the rest: the queue)
 };
 
 template <int D, bool RAND, bool NCO, bool CS16>
@@ -632,8 +583,7 @@ hipError_t launch_v(const KernelTables &t, const Launch &L)
     if (grid > nframes) grid = nframes;
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), 0, L.s, reinterpret_cast<const int *>(L.d_in),
                        L.d_out, nframes, t.tw_p1, t.tw_q1[D], t.rec_f, t.rec_i[D], t.tw4096, L.pq, L.tunebin, L.oa,
-                       L.nco, L.wq, frame_schedule_static(nframes, L.static_pct),
-                       occ == 4 && grid == cus * occ ? L.slotw : 0u);
+                       L.nco, occ == 4 && grid == cus * occ ? L.slotw : 0u);
     return hipGetLastError();
 }
 
@@ -664,13 +614,11 @@ hipError_t launch_build_split_filter(const KernelTables &t, int d, int tunebin, 
 
 hipError_t launch_frames_persistent(const KernelTables &t, int d, const int16_t *d_in, int nblk, void *d_out,
                                     const float4 *pq, int tunebin, int lsb, int rand, int cs16, float cs16_scale,
-                                    const float2 *nco_starts, const float2 *nco_trig, unsigned *wq, int slot_weights,
-                                    int static_pct, int device, hipStream_t s)
+                                    const float2 *nco_starts, const float2 *nco_trig, int slot_weights, int device,
+                                    hipStream_t s)
 {
-    if (static_pct < 0 || static_pct > 100) return hipErrorInvalidValue;
     const Launch L{d_in, nblk, d_out, pq, tunebin, device, s, OutArgs{lsb ? 0x80000000u : 0u, cs16_scale},
-                   NcoArgs{nco_starts, nco_trig}, wq, slot_weights && d >= 0 && d <= 6 ? kSlotWeights[d] : 0u,
-                   static_pct};
+                   NcoArgs{nco_starts, nco_trig}, slot_weights && d >= 0 && d <= 6 ? kSlotWeights[d] : 0u};
     const bool f = cs16 != 0;
     switch (d) {
     case 0: return launch_d<0>(t, L, rand, f);

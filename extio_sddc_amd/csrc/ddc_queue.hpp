@@ -17,7 +17,9 @@ namespace {
 // [slot_split(ns, G, w), slot_split(ns, G, w + 1)), with shares weighted by its slot's measured
 // speed (slotw; equal shares when slotw = 0 or the launch is not at full residency).  Frames
 // [ns, nframes) are handed out one at a time by a dynamic queue, which absorbs what the weights do
-// not predict and ends the launch frame-granular.  ns = nframes (d >= 3): no queue at all.
+// not predict and ends the launch frame-granular (the FS kernel, d = 0).  The persistent kernel
+// (d >= 1) uses the weighted split alone: there the queue's per-frame cost was larger than the
+// imbalance it removed (ddc_persistent.hip).
 //
 // The queue: 8 shards of consecutive frames (one counter each, on its own 64-B line); a workgroup
 // starts on shard blockIdx % 8 (its XCD under round-robin placement: neighbouring frames, which
@@ -125,8 +127,8 @@ struct FsQueue {
 // A workgroup's frame sequence: its static range, then the queue.  Worked by the queue wave only
 // (all bookkeeping wave-uniform, scalar).  LA: lookahead, the number of frames known ahead of the
 // current one (1: the FS kernel, which learns frame j + 1 at frame j's inverse pass 0; 2: the
-// persistent kernel, which prefetches frame j + 1 at frame j's top and learns frame j + 2 in
-// frame j's middle).
+// persistent kernel's form, which prefetches frame j + 1 at frame j's top and learns frame j + 2
+// in frame j's middle; measured and retired there, kept in tests/test_queue_model.py).
 template <int LA>
 struct FrameSchedule {
     FsQueue q;

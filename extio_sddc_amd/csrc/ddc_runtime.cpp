@@ -231,11 +231,8 @@ struct sddc_ddc {
     static constexpr int kQueueSlots = 64;
     unsigned *d_queue = nullptr;
     int queue_slot = 0;
-    int slot_weights = sddc::kSlotWeighting;    // d >= 3: slot-weighted static split (ddc_queue.hpp)
-    int fs_static_pct = sddc::kFsStaticPct;
-    int p_static_pct[SDDC_DDC_NDEC] = {sddc::kPStaticPct[0], sddc::kPStaticPct[1], sddc::kPStaticPct[2],
-                                       sddc::kPStaticPct[3], sddc::kPStaticPct[4], sddc::kPStaticPct[5],
-                                       sddc::kPStaticPct[6]};   // the persistent kernel's, per d (d <= 2)   // the d = 0 kernel's static share of frames (ddc_queue.hpp)
+    int slot_weights = sddc::kSlotWeighting;    // the persistent kernel's slot-weighted split (ddc_queue.hpp)
+    int fs_static_pct = sddc::kFsStaticPct;   // the d = 0 kernel's static share of frames (ddc_queue.hpp)
     hipStream_t q_s[kQueueSlots] = {};
     bool q_used[kQueueSlots] = {};
     bool q_dirty[kQueueSlots] = {};
@@ -747,13 +744,6 @@ static hipError_t launch_single_impl(sddc_ddc_t *h, const int16_t *d_in, int nbl
     } else if (hipError_t e = order_after_build(h, h->pq_s, s); e != hipSuccess) {
         return e;
     }
-    const bool persistent = !(h->d == 0 && h->variant >= 4 && h->variant <= 7);
-    unsigned *wq = nullptr;
-    int qi = -1;
-    if (persistent) {
-        hipError_t e = next_queue_slot(h, s, &wq, &qi);
-        if (e != hipSuccess) return e;
-    }
     hipError_t e = h->d == 0 && h->variant == 7
         ? V->frames_inplace(h->tables, d_in, nblk, d_out, h->d_pq, h->tunebin, h->lsb, h->rand,
                             h->out_fmt == SDDC_DDC_FMT_CS16, h->cs16_scale, nco_starts, nco_trig, h->device, s)
@@ -769,8 +759,7 @@ static hipError_t launch_single_impl(sddc_ddc_t *h, const int16_t *d_in, int nbl
                                         h->device, s)
         : sddc::launch_frames_persistent(h->tables, h->d, d_in, nblk, d_out, h->d_pq, h->tunebin, h->lsb, h->rand,
                                          h->out_fmt == SDDC_DDC_FMT_CS16, h->cs16_scale, nco_starts, nco_trig,
-                                         wq, h->slot_weights, h->p_static_pct[h->d], h->device, s);
-    if (qi >= 0) queue_slot_launched(h, qi, s, e);
+                                         h->slot_weights, h->device, s);
     if (e != hipSuccess) return e;
     return h->readers.record(s);
 }
@@ -818,10 +807,6 @@ int sddc_ddc_internal_set_param(sddc_ddc_t *h, int param, int value)
     if (!h) return fail(SDDC_ERR_ARG, "null handle");
     std::lock_guard<std::mutex> lk(h->mu);
     switch (param) {
-    case SDDC_DDC_PARAM_P_STATIC_PCT:
-        if (value < 0 || value > 100) return fail(SDDC_ERR_ARG, "static share %d outside 0..100", value);
-        for (int dd = 0; dd <= 2; dd++) h->p_static_pct[dd] = value;
-        return SDDC_OK;
     case SDDC_DDC_PARAM_SLOT_WEIGHTS:
         h->slot_weights = value != 0;
         return SDDC_OK;

@@ -15,12 +15,10 @@ int sddc_ddc_internal_set_variant(sddc_ddc_t *h, int variant);
  * SDDC_DDC_PARAM_FS_STATIC_PCT = the d = 0 kernel's share of each workgroup's frames taken
  * statically before it draws from the dynamic queue (0..100, default kFsStaticPct). */
 #define SDDC_DDC_PARAM_FS_STATIC_PCT 1
-/* SDDC_DDC_PARAM_SLOT_WEIGHTS = 1: the persistent kernel splits its statically scheduled frames by
- * CU slot speed (kSlotWeights[d]), 0: equal contiguous ranges (default kSlotWeighting). */
+/* SDDC_DDC_PARAM_SLOT_WEIGHTS = 1: the persistent kernel splits the frames by CU slot speed
+ * (kSlotWeights[d]), 0: equal contiguous ranges (default kSlotWeighting). */
 #define SDDC_DDC_PARAM_SLOT_WEIGHTS 2
-/* SDDC_DDC_PARAM_P_STATIC_PCT = the persistent kernel's statically split share of the frames at
- * d <= 2 (0..100, default kPStaticPct[d]). */
-#define SDDC_DDC_PARAM_P_STATIC_PCT 3
+
 int sddc_ddc_internal_set_param(sddc_ddc_t *h, int param, int value);
 /* Diagnostic stamp buffers of -DSDDC_STAMPS builds (tools/fs_stamps.py); -1 in product builds. */
 int sddc_ddc_internal_fs_stamps(unsigned *host, int nwords, int *words_per_wave);
