@@ -124,6 +124,10 @@ def main():
               f"end: min {re_us.min():.1f} p10 {np.percentile(re_us, 10):.1f} p50 {np.median(re_us):.1f} "
               f"p90 {np.percentile(re_us, 90):.1f} max {re_us.max():.1f}")
         print(f"  frames per workgroup: min {fr[:, 0].min():.0f} p50 {np.median(fr[:, 0]):.0f} max {fr[:, 0].max():.0f}")
+        xcd = np.arange(len(re_us)) % 8   # blockIdx % 8: the XCD under round-robin placement
+        print("    end p50 by blockIdx % 8 (XCD): " + " ".join(f"{np.median(re_us[xcd == x]):.1f}" for x in range(8))
+              + f"; within slot 0, p10..p90 {np.percentile(re_us[:len(re_us) // 4], 10):.1f}.."
+              f"{np.percentile(re_us[:len(re_us) // 4], 90):.1f} us")
         hw = st[:, 0, 2 * SEGS + 6].astype(np.int64)
         tg = (hw >> 16) & 0xF   # HW_ID TG_ID (bits 19:16): the workgroup slot on its CU
         for q in range(4):
