@@ -197,7 +197,9 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
     // bit-identical, d = 4 unchanged (profiles/r02/ab/grp5_d5_6*.txt).  At
     // d = 4 the branches raise the kernel to 142 VGPRs (3 waves/SIMD, 9-13 % slower; held to 128
     // it spills), so d = 4 keeps dft16 (profiles/r02/ab/grp_partial_dft16*.txt).
-    constexpr bool GRP = PRUNE && NB == 2 && D >= 5;
+    // (round 4: re-measured at d = 4 after the tails and the queue's removal left it at 90 VGPRs:
+    // 111 VGPRs, still 4 waves/SIMD, +4 %, profiles/r04/ab/pruned_f2_d4.txt; so d >= 4)
+    constexpr bool GRP = PRUNE && NB == 2 && D >= 4;
     const bool need2 = ((mrel & 3) - 1u) <= 1u, need3 = (mrel & 3) >= 2;
     __shared__ __attribute__((aligned(16))) float2 lds[HALF];
     // pass-1 twiddle tables, copied once per workgroup: [15][16] forward, [15][S] inverse

@@ -7,7 +7,7 @@
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=${1:-$R/gpurun_out/e2e}; mkdir -p $O
-H=$R/oracle/_ref/radiohandler_harness
+H=${HARNESS:-$R/oracle/_ref/radiohandler_harness}   # HARNESS: a variant build of the harness
 test -x $H || { echo "missing $H (make -C oracle radiohandler)"; exit 2; }
 : > $O/benchmark_test.jsonl
 for be in hip cpu; do
