@@ -128,14 +128,6 @@ __device__ __forceinline__ void wg_pass(const float2 *src, float2 *dst, const fl
     }
 }
 
-// lane s of each quad (ctrl = quad_perm [s, s, s, s] = 0x55 s), both components
-template <int CTRL>
-__device__ __forceinline__ float2 quad_bcast(float2 v)
-{
-    return make_float2(__int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v.x), CTRL, 0xF, 0xF, true)),
-                       __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v.y), CTRL, 0xF, 0xF, true)));
-}
-
 template <int N, int P>
 __device__ __forceinline__ void tail_pass(float2 *sb, const float2 *twq, int t, float2 (&u)[8])
 {
@@ -388,7 +380,7 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
                 const __amdgpu_buffer_rsrc_t rpq = buf_rsrc(pqz);
                 float2 a[R0];
 #pragma unroll
-                for (int r = 0; r < (N == 512 ? 0 : R0); r++) {   // (d = 3: below, in butterfly order)
+                for (int r = 0; r < R0; r++) {
                     const bool wrap = (NT * r >= N / 2);
                     const int sh = NT * r - (wrap ? N : 0);
                     // branch-free: read a valid (wrapped) address, out-of-band bins have P = Q = 0;
@@ -438,40 +430,17 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
                     continue;
                 }
                 if constexpr (N == 512) {
-                    // d = 3: the 512 filtered bins go to LDS after the first radix-8 Stockham pass,
-                    // which every wave runs across its quads: thread t = 4 j + q holds inverse inputs
-                    // j + 64 (2 q) and j + 64 (2 q + 1) of butterfly j (the split recomputed for that
-                    // order, DPP broadcasts, the same dft8 as tail_pass) and keeps outputs 2 q, 2 q + 1,
-                    // i.e. slots 2 t, 2 t + 1; then wave 0 runs passes 1 and 2 (tail_pass) instead of
-                    // all three (wave 0's tail is the rest of the frame's critical path)
-                    float2 x[8], y[8];
-                    {
-                        const int j = t >> 2, q = t & 3;
-#pragma unroll
-                        for (int h = 0; h < 2; h++) {
-                            const int m = j + 64 * (2 * q + h);
-                            const int bin = tunebin + m - (m >= N / 2 ? N : 0);
-                            a[h] = split_pq(w0[bin & (HALF - 1)], w0[(HALF - bin) & (HALF - 1)], pqz[m]);
-                        }
-                        x[0] = quad_bcast<0x00>(a[0]);
-                        x[1] = quad_bcast<0x00>(a[1]);
-                        x[2] = quad_bcast<0x55>(a[0]);
-                        x[3] = quad_bcast<0x55>(a[1]);
-                        x[4] = quad_bcast<0xAA>(a[0]);
-                        x[5] = quad_bcast<0xAA>(a[1]);
-                        x[6] = quad_bcast<0xFF>(a[0]);
-                        x[7] = quad_bcast<0xFF>(a[1]);
-                        dft8<+1>(x, y);
-                        a[0] = q == 0 ? y[0] : q == 1 ? y[2] : q == 2 ? y[4] : y[6];
-                        a[1] = q == 0 ? y[1] : q == 1 ? y[3] : q == 2 ? y[5] : y[7];
-                    }
+                    // d = 3: the 512 filtered bins (inverse input m = t + 256 r) go to LDS, and wave 0
+                    // runs the inverse as three radix-8 Stockham passes (tail_pass) instead of the
+                    // radix-2 pass on every thread and two radix-16 passes on 32 lanes
                     ST_SYNC(6);   // every wave's Z reads are done
 #pragma unroll
-                    for (int r = 0; r < R0; r++) w1[tail_swz<N>(2 * t + r)] = a[r];
+                    for (int r = 0; r < R0; r++) w1[tail_swz<N>(t + NT * r)] = a[r];
                     ST_SYNC(7);
                     if (t < 64) {
                         float2 v8[8];
                         const float2 *twq = twl + 15 * 16;
+                        tail_pass<N, 0>(w1, twq, t, v8);
                         tail_pass<N, 1>(w1, twq, t, v8);
                         tail_pass<N, 2>(w1, twq, t, v8);
                         tail_emit<N, NCO, CS16>(out, oblk + emit_base<N>(kc), kc, t, v8, oa, nco);
@@ -542,37 +511,19 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
             }
         } else {
             // ---- N <= 256: the N filtered bins (split x filter), one per thread ----
-            // d = 4 (N = 256): thread t takes inverse input m = (t >> 2) + 64 (t & 3), so that each
-            // quad holds one butterfly of the first radix-4 Stockham pass (inputs j + 64 r), which
-            // every wave then runs across its quads (DPP broadcasts, the same dft4 as tail_pass, so
-            // bit-identical) instead of wave 0 alone: pass 0's output 4 j + r is thread t's own
-            // slot.  Wave 0's tail is the rest of the frame's critical path (stamps: the other
-            // waves wait ~1.9k cycles for it at the next frame's first barrier).
-            constexpr bool Q0 = N == 256;
             float2 tv = make_float2(0.f, 0.f);
             if (t < N) {
-                const int m = Q0 ? (t >> 2) + (N / 4) * (t & 3) : t;
+                const int m = t;
                 const int bin = tunebin + m - (m >= N / 2 ? N : 0);
                 tv = split_pq(w0[bin & (HALF - 1)], w0[(HALF - bin) & (HALF - 1)], pqz[m]);
             }
-            if constexpr (Q0) {
-                float2 a[4], y[4];
-                a[0] = quad_bcast<0x00>(tv);
-                a[1] = quad_bcast<0x55>(tv);
-                a[2] = quad_bcast<0xAA>(tv);
-                a[3] = quad_bcast<0xFF>(tv);
-                dft4<+1>(a, y);
-                const int r = t & 3;
-                tv = r == 0 ? y[0] : r == 1 ? y[1] : r == 2 ? y[2] : y[3];
-            }
-            // the N filtered bins (d = 4: after pass 0) to sb, then wave 0 runs the inverse as
-            // Stockham passes
+            // the N filtered bins to sb, then wave 0 runs the inverse as Stockham passes
             if (t < N) sb[tail_swz<N>(t)] = tv;
             ST_SYNC(6);
             if (t < 64) {
                 float2 u[8];
                 const float2 *twq = twl + 15 * 16;
-                if constexpr (!Q0) tail_pass<N, 0>(sb, twq, t, u);
+                tail_pass<N, 0>(sb, twq, t, u);
                 tail_pass<N, 1>(sb, twq, t, u);
                 tail_pass<N, 2>(sb, twq, t, u);
                 if constexpr (tail_passes<N>() == 4) tail_pass<N, 3>(sb, twq, t, u);

@@ -44,7 +44,12 @@ static constexpr int kBlock = 65536;     // transferSamples, config.h:80-81
 // race (the reference reads it unsynchronised, impl.hpp:15; found by the TSan build).
 bool fft_mt_r2iq::on() const { return __atomic_load_n(&r2iqOn, __ATOMIC_ACQUIRE); }
 void fft_mt_r2iq::set_on(bool v) { __atomic_store_n(&r2iqOn, v, __ATOMIC_RELEASE); }
-static constexpr int kMaxBatch = 16;     // input blocks per GPU call (<= half the 32-transfer queue)
+// input blocks per GPU call: the blocks already queued in the 32-transfer ring (config.h:46), up
+// to 28, leaving the producer 4 free slots while the batch is copied.  At real-time rates the
+// queue holds a block or two and batches stay small; in the saturated benchmark_test procedure
+// 28 runs +21-27 % faster than 16 at decimate 0 (6.47 vs 5.09 GS/s input at 64 MHz,
+// profiles/r04/e2e/benchmark_test_maxbatch*.jsonl)
+static constexpr int kMaxBatch = 28;
 
 // The contiguous storage behind a ring's slots (ringbuffer::setBlockSize allocates all
 // slots in one array, Core/dsp/ringbuffer.h:150-165): walk peekReadPtr over one period.
