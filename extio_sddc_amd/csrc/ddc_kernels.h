@@ -69,7 +69,6 @@ struct KernelTables {
 // coefficients of (d, tunebin), HALF >> d float4, built by launch_build_split_filter.
 // nco_starts/nco_trig: fused fine-tune NCO tables (fine_tune.h), or nullptr for none.
 // cs16: write saturate(rint(x * cs16_scale)) int16 (I, Q) pairs instead of complex float.
-// wq: a zeroed dynamic-frame-queue slot (kFsQueueWords unsigned words), left zeroed.
 hipError_t launch_frames_persistent(const KernelTables &t, int d, const int16_t *d_in, int nblk,
                                     void *d_out, const float4 *pq, int tunebin, int lsb, int rand,
                                     int cs16, float cs16_scale, const float2 *nco_starts,
