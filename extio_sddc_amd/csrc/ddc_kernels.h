@@ -77,9 +77,11 @@ hipError_t launch_frames_persistent(const KernelTables &t, int d, const int16_t 
 // (kSlotWeights[d]: slot 0 in the low byte; ddc_queue.hpp slot_split), 0: equal contiguous
 // ranges.  The frames per slot of a balanced (queue-fed) run gave the weights: d = 1 29 / 25 /
 // 19 / 15, d = 4 27 / 24 / 20 / 16, tuned at d >= 3 to 29 / 25 / 20 / 15 (+3-6 %,
-// profiles/r04/ab/slot_weights_d3_6.txt).
+// profiles/r04/ab/slot_weights_d3_6.txt; the four slots then end within 1 us of each other,
+// stamps_p_d4_final_by_slot.txt) and at d <= 2 to 31 / 26 / 18 / 13 (d = 1 +4 %, d = 2 +2 %,
+// slot_weights_tuning_d1_6.txt).
 constexpr unsigned slot_weights4(unsigned a, unsigned b, unsigned c, unsigned e) { return a | (b << 8) | (c << 16) | (e << 24); }
-constexpr unsigned kSlotWeights[7] = {slot_weights4(29, 25, 19, 15), slot_weights4(29, 25, 19, 15), slot_weights4(29, 25, 19, 15),
+constexpr unsigned kSlotWeights[7] = {slot_weights4(31, 26, 18, 13), slot_weights4(31, 26, 18, 13), slot_weights4(31, 26, 18, 13),
                                       slot_weights4(29, 25, 20, 15), slot_weights4(29, 25, 20, 15),
                                       slot_weights4(29, 25, 20, 15), slot_weights4(29, 25, 20, 15)};
 constexpr int kSlotWeighting = 1;
