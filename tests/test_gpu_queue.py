@@ -1,15 +1,19 @@
-"""The dynamic frame queue's path against the oracle at headline size (pytest -m gpu).
+"""The headline-size frame schedules against the oracle (pytest -m gpu).
 
-The single-channel kernels hand frames out from a device-scope queue (ddc_queue.hpp) once a
-launch has more frames than resident workgroups: frames = 11 * nblk against CUs x 4 = 1024
-workgroups.  The small-batch parity tests (test_gpu_parity.py, 1-5 blocks) give every workgroup
-one static frame, so they never take a ticket, hop a shard or run the d = 1, 2 two-static-frame
-start.  Here the launches are 256 and 2048 blocks (the BASELINE C2 batch) into NaN-filled
-outputs, and the HIP output is compared with the f64 oracle (fft_mt_r2iq_impl.hpp:84-138):
+A launch has frames = 11 * nblk against CUs x 4 = 1024 resident workgroups.  Since round 4 both
+single-channel kernels split a full-residency launch's frames statically, each workgroup a
+contiguous range sized by its CU slot's speed (ddc_queue.hpp slot_split), and the FS kernel can
+still hand out the rest of its frames from the device-scope queue (SDDC_DDC_PARAM_FS_STATIC_PCT
+< 100: tickets, shard hops, the dry-shard scan).  The small-batch parity tests
+(test_gpu_parity.py, 1-5 blocks) never reach either: there every workgroup has one frame.
+Here the launches are 256 and 2048 blocks (the BASELINE C2 batch) into NaN-filled outputs, and
+the HIP output is compared with the f64 oracle (fft_mt_r2iq_impl.hpp:84-138):
   - every block of the 256-block launches and of the 2048-block d = 0 launch (the headline);
   - at 2048 blocks for d = 1, 2, 4: 2-block windows at the first, middle and last frame of each
-    of the queue's 8 shards, the last block and random blocks, each window fed its real
-    4096-sample history from the stream.
+    of 8 equal stretches of the stream, the last block and random blocks, each window fed its
+    real 4096-sample history from the stream;
+  - every schedule computes each frame the same way, so the queue-fed FS launches (static share
+    0 % and 40 %) and the equal split must match the default bit for bit.
 Plus the queue ring's reuse across streams (more than kQueueSlots = 64 launches over three
 streams, one of them backed up) and a table rebuild on one stream read by a launch on another.
 """
@@ -220,3 +224,40 @@ def test_table_rebuild_seen_by_other_stream(torch_dev, ddc, oracle, H, d, tb0, t
         yy = y.cpu().numpy().view(np.complex64)
         assert oracle.max_rel_err(yy, r) <= TOL
     assert torch.equal(ya, yb)
+
+
+P_FS_STATIC_PCT, P_SLOT_WEIGHTS = 1, 2   # sddc_ddc_internal.h SDDC_DDC_PARAM_*
+
+
+def _set_param(r, param, value):
+    import ctypes
+    from extio_sddc_amd import _lib
+    f = r._L.sddc_ddc_internal_set_param
+    f.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+    f.restype = ctypes.c_int
+    _lib.check(f(r._h, param, value))
+
+
+@pytest.mark.parametrize("d,param,values", [(0, P_FS_STATIC_PCT, (100, 40, 0)), (1, P_SLOT_WEIGHTS, (1, 0)),
+                                            (4, P_SLOT_WEIGHTS, (1, 0))])
+def test_schedules_bit_identical(torch_dev, d, param, values):
+    """the FS queue at static shares 40 % and 0 % (every frame from the queue), and the equal
+    split instead of the slot-weighted one, against the default, 2048 blocks, NaN-filled"""
+    torch = torch_dev
+    from extio_sddc_amd import R2iq, output_samples
+    nblk = 2048
+    g = torch.Generator(device="cuda").manual_seed(0x5DDC + d)
+    d_in = torch.randint(-32768, 32767, (HIST + nblk * BLOCK,), dtype=torch.int16, device="cuda", generator=g)
+    outs = []
+    with R2iq(gain=1.0, device=0) as r:
+        r.setDecimate(d)
+        r.setTuneBin(1024)
+        for v in values:
+            _set_param(r, param, v)
+            out = torch.full((output_samples(d, nblk) * 2,), float("nan"), dtype=torch.float32, device="cuda")
+            r.process_device(d_in, nblk, out)
+            torch.cuda.synchronize()
+            outs.append(out.view(torch.int32).cpu().numpy())
+    assert not np.any(np.isnan(outs[0].view(np.float32))), "frames left unwritten"
+    for o in outs[1:]:
+        np.testing.assert_array_equal(o, outs[0])
