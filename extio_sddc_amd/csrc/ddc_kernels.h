@@ -99,7 +99,7 @@ hipError_t launch_build_fs_tables(const KernelTables &t, int tunebin, float4 *pq
 // from the queue (ddc_queue.hpp FrameSchedule); kFsStaticPct by default.
 constexpr int kFsQueueWords = 16 * 9;
 constexpr int kFsStaticPct = 100;   // (85 / 95 / 100 %: 0.240 / 0.238 / 0.235 ms, profiles/r04/ab/fs_static_share_d0.txt)
-constexpr unsigned kFsSlotWeights = slot_weights4(32, 26, 18, 12);   // (per-slot ends, fs_slot_weights_d0.txt)
+constexpr unsigned kFsSlotWeights = slot_weights4(31, 26, 18, 13);   // (between the boxes' optima, fs_slot_weights_d0.txt)
 hipError_t launch_frames_fs(const KernelTables &t, const int16_t *d_in, int nblk, void *d_out, const float4 *pqf,
                             const float2 *fsl, int tunebin, int lsb, int rand, int cs16, float cs16_scale,
                             const float2 *nco_starts, const float2 *nco_trig, unsigned *wq, int static_pct,
