@@ -135,6 +135,11 @@ def main():
             print(f"    blockIdx quarter {q}: end p50 {np.median(re_us[sel]):.1f} us, frames p50 {np.median(fr[sel, 0]):.0f}"
                   f"; HW slot {q}: {int(np.sum(tg == q))} workgroups, end p50 "
                   f"{np.median(re_us[tg == q]) if np.any(tg == q) else float('nan'):.1f} us")
+        for wv in range(4):   # HW_ID SIMD_ID (bits 5:4) of wave wv, over the workgroups
+            simd = (st[:, wv, 2 * SEGS + 6].astype(np.int64) >> 4) & 3
+            print(f"    wave {wv}: SIMD 0..3 " + " ".join(str(int(np.sum(simd == s))) for s in range(4))
+                  + " workgroups; wave - SIMD mod 4: " + " ".join(str(int(np.sum((wv - simd) % 4 == s)))
+                                                                 for s in range(4)))
         lo = 4 * (which - 1)
         rows = []
         for i in range(SEGS):
