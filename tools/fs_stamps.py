@@ -159,6 +159,7 @@ def main():
         res[os.path.basename(lib)] = {"ms": ms, "clock_GHz": clk, "build": which, "kernel": args.kernel, "d": args.d,
                                       "wg_end_us": {"min": float(re_us.min()), "p50": float(np.median(re_us)),
                                                     "max": float(re_us.max())},
+                                      "xcd_end_p50_us": [float(np.median(re_us[xcd == x])) for x in range(8)],
                                       "rows": [{"seg": i, "what": n, "work_cycles_per_frame_wave0..3": wk,
                                                 "barrier_wait_cycles_per_frame_wave0..3": wt}
                                                for i, n, wk, wt in rows]}
