@@ -480,10 +480,11 @@ def main() -> None:
     ap.add_argument("--tunebin", type=int, default=1024)
     ap.add_argument("--nblk", type=int, default=2048, help="blocks of 65536 per step per GPU")
     ap.add_argument("--mode", choices=["single", "channels"], default="single")
-    ap.add_argument("--streams", type=int, default=2,
+    ap.add_argument("--streams", type=int, default=1,
                     help="single mode: consecutive batches alternate over this many HIP streams (each with its "
-                         "own output buffer), so one batch's launch tail overlaps the next batch's start "
-                         "(DESIGN.md §5); the roofline comes from a separate single-stream run of the same steps")
+                         "own output buffer), so one batch's launch tail overlaps the next batch's start; the "
+                         "roofline then comes from a separate single-stream run of the same steps.  Default 1 "
+                         "since round 5: with the static split two streams measured slower (DESIGN.md §5)")
     ap.add_argument("--channels", type=int, default=1024)
     ap.add_argument("--bcast", choices=["sag", "bcast"], default="sag",
                     help="C5 input broadcast for N > 1: scatter + all-gather over all links (sag) or one "

@@ -69,6 +69,18 @@ __device__ __forceinline__ void split_dpp2(float2 &fa, float2 &fb, float2 za, fl
         : "v"(za.x), "v"(za.y), "v"(zb.x), "v"(zb.y), "v"(qa.z), "v"(qa.w), "v"(qb.z), "v"(qb.w));
 }
 
+// one half of split_dpp2: f += conj(z of the partner lane) q
+__device__ __forceinline__ void split_dpp1(float2 &f, float2 z, float4 q)
+{
+    asm("s_nop 1\n\t"
+        "v_fmac_f32_dpp %0, %2, %4 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %0, %3, %5 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %1, %2, %5 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %1, -%3, %4 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf"
+        : "+v"(f.x), "+v"(f.y)
+        : "v"(z.x), "v"(z.y), "v"(q.z), "v"(q.w));
+}
+
 // Zk P (own registers)
 __device__ __forceinline__ float2 zk_p(float2 zk, float4 c)
 {
@@ -117,11 +129,25 @@ constexpr int kQWave = 3;
 // 32-lane group.  The other exchanges use the first 4096 slots with XOR keys.
 constexpr int kFsLds = HALF + HALF / 16;
 
-template <bool RAND, bool LSB, bool NCO, bool CS16>
+// the frame schedules (ddc_queue.hpp): the slot-weighted static split alone, the static prefix +
+// dynamic queue (round 3/4), work stealing over the static split (default since round 5)
+enum { kSchedStatic = 0, kSchedQueue = 1, kSchedSteal = 2 };
+template <int SCHED> struct SchedOf { using T = StealSchedule; };
+template <> struct SchedOf<kSchedStatic> { using T = StaticSchedule; };
+template <> struct SchedOf<kSchedQueue> { using T = FrameSchedule<1>; };
+
+// ZR: whole rows of the inverse input known zero for this tune bin (the reference's zero fill,
+// impl.hpp:91-96): 4 = rows 12..15 (bins 3072..4095, tb <= 1024), -4 = rows 0..3 (bins 0..1023,
+// tb >= 3072), 0 = none.  Their (P, Q) loads and split FMAs are skipped and I0's first radix-4s
+// take only the live rows (dft16z).
+template <int ZR>
+__device__ __forceinline__ constexpr bool zrow(int k) { return ZR > 0 ? k >= 16 - ZR : ZR < 0 ? k < -ZR : false; }
+
+template <int SCHED, int ZR, bool RAND, bool LSB, bool NCO, bool CS16>
 __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
     const int *__restrict__ in32, void *__restrict__ out, int nframes, const float2 *__restrict__ tw_p1,
     const float2 *__restrict__ rec_f, const float4 *__restrict__ pqf, const float2 *__restrict__ fsl, int tunebin,
-    OutArgs oa, NcoArgs nco, unsigned *__restrict__ wq, int ns, unsigned slotw)
+    OutArgs oa, NcoArgs nco, unsigned *__restrict__ wq, int ns, unsigned slotw, int xmap, int minrem, int pub)
 {
     __shared__ __attribute__((aligned(16))) float2 lds[kFsLds];
     // F1 twiddles W_256^{s r} [15][16] (I1 conjugates them: at d = 0 its table is the same) and
@@ -135,10 +161,12 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
                   "four workgroups per CU");
 
     const int tid = (int)threadIdx.x;
-    const int w = (int)blockIdx.x;
+    // xmap (non-persistent grids): blockIdx b runs on XCD b % 8 under round-robin placement, and
+    // takes frame range (b % 8) G / 8 + b / 8, so that each XCD walks a contiguous stretch
+    const int w = xmap ? (int)(blockIdx.x & 7u) * (int)(gridDim.x >> 3) + (int)(blockIdx.x >> 3) : (int)blockIdx.x;
     constexpr int QLANE = 64 * kQWave;
     const bool qw = __builtin_amdgcn_readfirstlane(tid >> 6) == kQWave;
-    FrameSchedule<1> fsch;
+    typename SchedOf<SCHED>::T fsch;
     int x[16];
     {
         // every wave knows the first frame (it is static unless the batch is small): its input
@@ -148,7 +176,8 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
         if (f0s >= 0) load_frame(in32, f0s / FRAMES, f0s % FRAMES, x);
         if (qw) {
             int f0[1];
-            fsch.init(wq, nframes, ns, w, G, slotw, f0);
+            if constexpr (SCHED == kSchedSteal) fsch.init(wq, nframes, ns, w, G, slotw, f0, minrem, pub);
+            else fsch.init(wq, nframes, ns, w, G, slotw, f0);
             if (tid == QLANE) s_next = f0[0];
         }
         for (int i = tid; i < 15 * 16; i += NT) twl[i] = tw_p1[i];
@@ -166,7 +195,8 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
     ST_INIT();
 
     while (f >= 0) {
-        if (qw) fsch.peek();
+        if constexpr (SCHED != kSchedSteal)
+            if (qw) fsch.peek();
         // opaque per-frame copies of the thread index and column: without them the compiler
         // hoists every loop-invariant LDS address out of the frame loop and spills them
         int z = 0;
@@ -214,6 +244,8 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
 #pragma unroll
         for (int r = 0; r < 16; r++) st_row(lds, xa1, r, 16, v[r]);   // element 256 (t >> 4) + 16 r + (x15 ^ r)
         ST_SYNC(3);
+        if constexpr (SCHED == kSchedSteal)
+            if (qw) fsch.peek();
         // ---- F2 (R16, NS256) on column c: Z[c + 256 k] in v[k] ----
         // The split's (P, Q) loads (bin pairs p, 15 - p) run a pair ahead of their use, the first
         // issued before F2 so that its reads and arithmetic cover the L2 latency (an empty asm
@@ -222,8 +254,8 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
         const __amdgpu_buffer_rsrc_t rpq = buf_rsrc(pqf + z);
         const unsigned t16 = 16u * (unsigned)t;
         float4 qa[8], qb[8];
-        qa[0] = buf_load16(rpq, t16, 0);
-        qb[0] = buf_load16(rpq, t16, 16u * NT * 15);
+        if constexpr (!zrow<ZR>(0)) qa[0] = buf_load16(rpq, t16, 0);
+        if constexpr (!zrow<ZR>(15)) qb[0] = buf_load16(rpq, t16, 16u * NT * 15);
         asm volatile("" ::: "memory");
         {
             float2 a[16];
@@ -242,14 +274,24 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
 #pragma unroll
                 for (int p = 0; p < 8; p++) {
                     if (p + 1 < 8) {
-                        qa[p + 1] = buf_load16(rpq, t16, 16u * NT * (p + 1));
-                        qb[p + 1] = buf_load16(rpq, t16, 16u * NT * (14 - p));
+                        if (!zrow<ZR>(p + 1)) qa[p + 1] = buf_load16(rpq, t16, 16u * NT * (p + 1));
+                        if (!zrow<ZR>(14 - p)) qb[p + 1] = buf_load16(rpq, t16, 16u * NT * (14 - p));
                         asm volatile("" ::: "memory");
                     }
-                    float2 fa = zk_p(v[p], qa[p]), fb = zk_p(v[15 - p], qb[p]);
-                    split_dpp2(fa, fb, v[15 - p], v[p], qa[p], qb[p]);
-                    a[p] = fa;
-                    a[15 - p] = fb;
+                    if (zrow<ZR>(15 - p)) {   // row 15 - p zero: row p's half alone
+                        float2 fa = zk_p(v[p], qa[p]);
+                        split_dpp1(fa, v[15 - p], qa[p]);
+                        a[p] = fa;
+                    } else if (zrow<ZR>(p)) {
+                        float2 fb = zk_p(v[15 - p], qb[p]);
+                        split_dpp1(fb, v[p], qb[p]);
+                        a[15 - p] = fb;
+                    } else {
+                        float2 fa = zk_p(v[p], qa[p]), fb = zk_p(v[15 - p], qb[p]);
+                        split_dpp2(fa, fb, v[15 - p], v[p], qa[p], qb[p]);
+                        a[p] = fa;
+                        a[15 - p] = fb;
+                    }
                 }
             } else {
                 // wave 0: lanes 0 (column 0: mirror of register k is its own (16 - k) mod 16) and
@@ -258,13 +300,14 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
 #pragma unroll
                 for (int p = 0; p < 8; p++) {
                     if (p + 1 < 8) {
-                        qa[p + 1] = buf_load16(rpq, t16, 16u * NT * (p + 1));
-                        qb[p + 1] = buf_load16(rpq, t16, 16u * NT * (14 - p));
+                        if (!zrow<ZR>(p + 1)) qa[p + 1] = buf_load16(rpq, t16, 16u * NT * (p + 1));
+                        if (!zrow<ZR>(14 - p)) qb[p + 1] = buf_load16(rpq, t16, 16u * NT * (14 - p));
                         asm volatile("" ::: "memory");
                     }
 #pragma unroll
                     for (int h = 0; h < 2; h++) {
                         const int kk = h ? 15 - p : p;
+                        if (zrow<ZR>(kk)) continue;
                         const float4 q = h ? qb[p] : qa[p];
                         const float2 vm = v[15 - kk], v0m = v[(16 - kk) & 15];
                         float2 zc = make_float2(dpp_partner(vm.x), dpp_partner(vm.y));
@@ -274,7 +317,7 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
                     }
                 }
             }
-            dft16<+1>(a, u);
+            dft16z<+1, ZR>(a, u);
         }
         ST_SYNC(4);   // every wave's F2 reads are done
         {
@@ -348,11 +391,14 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
             default: emit_frame_q<3, LSB, NCO, CS16>(out, fb, kc, t, u, oa, nco); break;
             }
         }
+        if constexpr (SCHED == kSchedSteal)
+            if (qw) fsch.take_late();
         ST_FRAME_END();
         f = fn;
     }
     ST_WRITE(g_fs_stamps, w, tid);
-    if (tid == QLANE) fs_queue_done(wq, (unsigned)gridDim.x);
+    if constexpr (SCHED == kSchedQueue)
+        if (tid == QLANE) fs_queue_done(wq, (unsigned)gridDim.x);
 }
 
 // FS tables of one tunebin: pqf[l + 256 k] = (P, Q) of bin b = kFsPerm[l] + 256 k (inverse input
@@ -387,35 +433,84 @@ __global__ void build_fs_tables_kernel(const float2 *__restrict__ hsel0, const f
     }
 }
 
-template <bool RAND, bool LSB, bool NCO, bool CS16>
-hipError_t launch_fs_v(const KernelTables &t, const int16_t *d_in, int nblk, void *d_out, const float4 *pqf,
+template <int SCHED, int ZR, bool RAND, bool LSB, bool NCO, bool CS16>
+hipError_t launch_fs_s(const KernelTables &t, const int16_t *d_in, int nblk, void *d_out, const float4 *pqf,
                        const float2 *fsl, int tunebin, const OutArgs &oa, const NcoArgs &nco, unsigned *wq,
-                       int static_pct, int device, hipStream_t s)
+                       const FsSched &fs, int device, hipStream_t s)
 {
-    auto kern = r2iq_fs_kernel<RAND, LSB, NCO, CS16>;
+    auto kern = r2iq_fs_kernel<SCHED, ZR, RAND, LSB, NCO, CS16>;
+    const int static_pct = SCHED == kSchedQueue ? fs.static_pct : 100, fpw = fs.fpw;
     int occ = 0, cus = 0;
     hipError_t e = launch_geometry(t.lc, reinterpret_cast<const void *>(kern), NT, device, &occ, &cus);
     if (e != hipSuccess) return e;
     const int nframes = nblk * FRAMES;
     int grid = cus * occ;
     if (grid > nframes) grid = nframes;
-    const int ns = frame_schedule_static(nframes, static_pct);
-    const unsigned slotw = occ == 4 && grid == cus * occ ? kFsSlotWeights : 0u;
+    int ns = frame_schedule_static(nframes, static_pct);
+    unsigned slotw = occ == 4 && grid == cus * occ ? kFsSlotWeights : 0u;
+    int xmap = 0;
+    if (fpw > 0) {   // non-persistent: fpw frames per workgroup, the hardware dispatcher balances
+        grid = (nframes + fpw - 1) / fpw;
+        ns = nframes;
+        slotw = 0u;
+        xmap = (grid & 7) == 0 && grid * fpw == nframes;
+    }
+    int minrem = fs.minrem;
+    // a steal slot counts at most kStealMaxRange frames of a range, for at most kFsStealMax
+    // workgroups (the largest range of the weighted split is below 2 nframes / G + 1); a launch
+    // past either runs the static split alone (minrem 0)
+    if (SCHED == kSchedSteal && (grid > kFsStealMax || 2LL * nframes / grid + 1 > kStealMaxRange)) minrem = 0;
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT), 0, s, reinterpret_cast<const int *>(d_in), d_out, nframes,
-                       t.tw_p1, t.rec_f, pqf, fsl, tunebin, oa, nco, wq, ns, slotw);
+                       t.tw_p1, t.rec_f, pqf, fsl, tunebin, oa, nco, wq, ns, slotw, xmap, minrem, fs.pub);
     return hipGetLastError();
+}
+
+// zero rows of the inverse input for tune bin tb (ZR of r2iq_fs_kernel): 4 when bins 3072..4095 are
+// out of band (tb <= 1024), -4 when bins 0..1023 are (tb >= 3072), else 0
+int fs_zero_rows(int tunebin) { return tunebin <= 1024 ? 4 : tunebin >= 3072 ? -4 : 0; }
+
+template <int ZR, bool RAND, bool LSB, bool NCO, bool CS16>
+hipError_t launch_fs_z(const KernelTables &t, const int16_t *d_in, int nblk, void *d_out, const float4 *pqf,
+                       const float2 *fsl, int tunebin, const OutArgs &oa, const NcoArgs &nco, unsigned *wq,
+                       const FsSched &fs, int device, hipStream_t s)
+{
+    if (fs.sched == kSchedStatic)
+        return launch_fs_s<kSchedStatic, ZR, RAND, LSB, NCO, CS16>(t, d_in, nblk, d_out, pqf, fsl, tunebin, oa, nco, wq, fs, device, s);
+    if constexpr (!RAND && !LSB && !NCO && !CS16) {
+        if (fs.sched == kSchedSteal)
+            return launch_fs_s<kSchedSteal, ZR, false, false, false, false>(t, d_in, nblk, d_out, pqf, fsl, tunebin, oa, nco, wq, fs, device, s);
+        if (fs.sched == kSchedQueue)
+            return launch_fs_s<kSchedQueue, ZR, false, false, false, false>(t, d_in, nblk, d_out, pqf, fsl, tunebin, oa, nco, wq, fs, device, s);
+    }
+    return hipErrorNotSupported;
+}
+
+// the schedule: every output configuration runs the static schedule (the default); work stealing
+// and the queue (A/B, tests) are built for the plain configuration only.  fs.zr: -1 picks the
+// tune bin's zero rows, 0 forces none (A/B)
+template <bool RAND, bool LSB, bool NCO, bool CS16>
+hipError_t launch_fs_v(const KernelTables &t, const int16_t *d_in, int nblk, void *d_out, const float4 *pqf,
+                       const float2 *fsl, int tunebin, const OutArgs &oa, const NcoArgs &nco, unsigned *wq,
+                       const FsSched &fs, int device, hipStream_t s)
+{
+    const int zr = fs.zr ? fs_zero_rows(tunebin) : 0;
+    if (zr == 4)
+        return launch_fs_z<4, RAND, LSB, NCO, CS16>(t, d_in, nblk, d_out, pqf, fsl, tunebin, oa, nco, wq, fs, device, s);
+    if (zr == -4)
+        return launch_fs_z<-4, RAND, LSB, NCO, CS16>(t, d_in, nblk, d_out, pqf, fsl, tunebin, oa, nco, wq, fs, device, s);
+    return launch_fs_z<0, RAND, LSB, NCO, CS16>(t, d_in, nblk, d_out, pqf, fsl, tunebin, oa, nco, wq, fs, device, s);
 }
 
 template <bool RAND, bool LSB>
 hipError_t launch_fs_rl(const KernelTables &t, const int16_t *d_in, int nblk, void *d_out, const float4 *pqf,
                         const float2 *fsl, int tunebin, bool cs16, const OutArgs &oa, const NcoArgs &nco,
-                        unsigned *wq, int static_pct, int device, hipStream_t s)
+                        unsigned *wq, const FsSched &fs, int device, hipStream_t s)
 {
     if (nco.starts)
-        return cs16 ? launch_fs_v<RAND, LSB, true, true>(t, d_in, nblk, d_out, pqf, fsl, tunebin, oa, nco, wq, static_pct, device, s)
-                    : launch_fs_v<RAND, LSB, true, false>(t, d_in, nblk, d_out, pqf, fsl, tunebin, oa, nco, wq, static_pct, device, s);
-    return cs16 ? launch_fs_v<RAND, LSB, false, true>(t, d_in, nblk, d_out, pqf, fsl, tunebin, oa, nco, wq, static_pct, device, s)
-                : launch_fs_v<RAND, LSB, false, false>(t, d_in, nblk, d_out, pqf, fsl, tunebin, oa, nco, wq, static_pct, device, s);
+        return cs16 ? launch_fs_v<RAND, LSB, true, true>(t, d_in, nblk, d_out, pqf, fsl, tunebin, oa, nco, wq, fs, device, s)
+                    : launch_fs_v<RAND, LSB, true, false>(t, d_in, nblk, d_out, pqf, fsl, tunebin, oa, nco, wq, fs, device, s);
+    return cs16 ? launch_fs_v<RAND, LSB, false, true>(t, d_in, nblk, d_out, pqf, fsl, tunebin, oa, nco, wq, fs, device, s)
+                : launch_fs_v<RAND, LSB, false, false>(t, d_in, nblk, d_out, pqf, fsl, tunebin, oa, nco, wq, fs, device, s);
 }
 
 }  // namespace
@@ -432,19 +527,19 @@ hipError_t launch_build_fs_tables(const KernelTables &t, int tunebin, float4 *pq
 
 hipError_t launch_frames_fs(const KernelTables &t, const int16_t *d_in, int nblk, void *d_out, const float4 *pqf,
                             const float2 *fsl, int tunebin, int lsb, int rand, int cs16, float cs16_scale,
-                            const float2 *nco_starts, const float2 *nco_trig, unsigned *wq, int static_pct,
+                            const float2 *nco_starts, const float2 *nco_trig, unsigned *wq, const FsSched &fs,
                             int device, hipStream_t s)
 {
     if (tunebin & 3) return hipErrorInvalidValue;
-    if (static_pct < 0 || static_pct > 100) return hipErrorInvalidValue;
+    if (fs.static_pct < 0 || fs.static_pct > 100 || fs.sched < 0 || fs.sched > 2) return hipErrorInvalidValue;
     const OutArgs oa{0u, cs16_scale};   // the sideband flip is a template parameter here
     const NcoArgs nco{nco_starts, nco_trig};
     const bool c = cs16 != 0;
     if (rand)
-        return lsb ? launch_fs_rl<true, true>(t, d_in, nblk, d_out, pqf, fsl, tunebin, c, oa, nco, wq, static_pct, device, s)
-                   : launch_fs_rl<true, false>(t, d_in, nblk, d_out, pqf, fsl, tunebin, c, oa, nco, wq, static_pct, device, s);
-    return lsb ? launch_fs_rl<false, true>(t, d_in, nblk, d_out, pqf, fsl, tunebin, c, oa, nco, wq, static_pct, device, s)
-               : launch_fs_rl<false, false>(t, d_in, nblk, d_out, pqf, fsl, tunebin, c, oa, nco, wq, static_pct, device, s);
+        return lsb ? launch_fs_rl<true, true>(t, d_in, nblk, d_out, pqf, fsl, tunebin, c, oa, nco, wq, fs, device, s)
+                   : launch_fs_rl<true, false>(t, d_in, nblk, d_out, pqf, fsl, tunebin, c, oa, nco, wq, fs, device, s);
+    return lsb ? launch_fs_rl<false, true>(t, d_in, nblk, d_out, pqf, fsl, tunebin, c, oa, nco, wq, fs, device, s)
+               : launch_fs_rl<false, false>(t, d_in, nblk, d_out, pqf, fsl, tunebin, c, oa, nco, wq, fs, device, s);
 }
 
 }  // namespace sddc

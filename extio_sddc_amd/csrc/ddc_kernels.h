@@ -97,12 +97,27 @@ hipError_t launch_build_fs_tables(const KernelTables &t, int tunebin, float4 *pq
 // zeroed again.  Launches that may run at the same time need different slots.
 // static_pct: the share (percent) of each workgroup's frames taken statically before it draws
 // from the queue (ddc_queue.hpp FrameSchedule); kFsStaticPct by default.
-constexpr int kFsQueueWords = 16 * 9;
+constexpr int kFsQueueLineWords = 16 * 9;                  // the dynamic queue's counters
+constexpr int kFsStealMax = 2048;                         // steal slots (2 words): workgroups per launch
+constexpr int kFsQueueWords = kFsQueueLineWords + 2 * kFsStealMax;
 constexpr int kFsStaticPct = 100;   // (85 / 95 / 100 %: 0.240 / 0.238 / 0.235 ms, profiles/r04/ab/fs_static_share_d0.txt)
 constexpr unsigned kFsSlotWeights = slot_weights4(31, 26, 18, 13);   // (between the boxes' optima, fs_slot_weights_d0.txt)
+// The FS kernel's frame schedule (ddc_queue.hpp): sched 0 the slot-weighted static split alone
+// (default; every output configuration), 2 work stealing, 1 the static prefix of static_pct
+// percent + the dynamic queue (1 and 2: the plain configuration only, A/B and tests).  fpw > 0: a
+// non-persistent grid of fpw frames per workgroup (A/B).  minrem: a thief steals only from ranges
+// with at least minrem unclaimed frames (0: none, the static split inside the stealing kernel).
+struct FsSched {
+    int sched = 0;
+    int static_pct = kFsStaticPct;
+    int fpw = 0;
+    int minrem = 1;
+    int pub = 0;   // frames at the end of each range open to thieves (0: all but the first two)
+    int zr = 1;    // skip the tune bin's whole zero rows of the inverse input (0: never; A/B)
+};
 hipError_t launch_frames_fs(const KernelTables &t, const int16_t *d_in, int nblk, void *d_out, const float4 *pqf,
                             const float2 *fsl, int tunebin, int lsb, int rand, int cs16, float cs16_scale,
-                            const float2 *nco_starts, const float2 *nco_trig, unsigned *wq, int static_pct,
+                            const float2 *nco_starts, const float2 *nco_trig, unsigned *wq, const FsSched &fs,
                             int device, hipStream_t s);
 
 // many-channel v2 (d = 4..6): persistent, forward once per (frame, 128-channel chunk)

@@ -4,6 +4,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include "ddc_device_io.hpp"
+
 namespace sddc {
 namespace {
 
@@ -31,7 +33,7 @@ namespace {
 // wq: this launch's slot of the handle's queue ring, zero at entry; the last workgroup to leave
 // clears it for the slot's next launch (the counters are touched only by device-scope atomics).
 constexpr int FS_SHARDS = 8;
-static_assert(kFsQueueWords == 16 * (FS_SHARDS + 1), "queue slot: one 64-B line per shard counter + the done count");
+static_assert(kFsQueueLineWords == 16 * (FS_SHARDS + 1), "queue slot: one 64-B line per shard counter + the done count");
 constexpr unsigned FS_OOB = 0x80000000u;   // a buffer offset past the queue slot's range
 
 // first frame of workgroup v (v = G: ns) of the slot-weighted static split of ns frames.
@@ -69,7 +71,7 @@ struct FsQueue {
     __device__ __forceinline__ int shard_lo(int s) const { return base + ((nd * s) >> 3); }
     __device__ __forceinline__ void init(unsigned *wq, int base_, int nd_, int home)
     {
-        rq = __builtin_amdgcn_make_buffer_rsrc(wq, (short)0, 4 * kFsQueueWords, 0x00020000);
+        rq = __builtin_amdgcn_make_buffer_rsrc(wq, (short)0, 4 * kFsQueueLineWords, 0x00020000);
         base = base_;
         nd = nd_;
         sh0 = home;
@@ -173,6 +175,198 @@ struct FrameSchedule {
     __device__ __forceinline__ void take()
     {
         if (rem <= 0) q.take();
+    }
+};
+
+// The static schedule: the slot-weighted split alone (no atomics).  Same interface as
+// FrameSchedule<1> and StealSchedule (init / peek / next / take), worked by the queue wave.
+struct StaticSchedule {
+    int nxt, end;
+    __device__ __forceinline__ void init(unsigned *, int, int ns, int w, int G, unsigned slotw, int (&f)[1])
+    {
+        const int a = slot_split(ns, G, w, slotw), b = slot_split(ns, G, w + 1, slotw);
+        f[0] = a < b ? a : -1;
+        nxt = a + 1;
+        end = b;
+    }
+    __device__ __forceinline__ void peek() {}
+    __device__ __forceinline__ int next() { return nxt < end ? nxt++ : -1; }
+    __device__ __forceinline__ void take() {}
+};
+
+// Work stealing (the FS kernel's default schedule, round 5).  Each workgroup owns the range
+// [a, b) of the slot-weighted split and claims its frames in order; a workgroup whose range is
+// exhausted steals single frames from the END of other ranges.  Per workgroup one 8-byte slot in
+// the launch's queue slot: the word (front << 16) | (kStealBias + end), front / end relative to a,
+// and a itself.
+//   owner claim:  old = atomic_add(word, 0x10000)  -> frame a + old.front   if old.front < old.end
+//   steal:        old = atomic_add(word, -1)       -> frame a + old.end - 1 if old.end - 1 >= old.front
+// Both are agent-scope atomics on one word, so every frame of a range is claimed exactly once
+// (an owner claim of x needs end > x, a steal of x leaves end = x; a steal of x needs front <= x,
+// an owner claim of x leaves front = x + 1; tests/test_queue_model.py drives this with random
+// interleavings).  A failed steal only lowers end further, which no claim can pass again; the bias
+// keeps end from borrowing into front (at most kStealBias failed steals per word).
+// Pipelining (the queue wave, like FrameSchedule): the claim that decides frame j + 2 is issued at
+// frame j's inverse pass 1 (take) and read at frame j + 1's I0 (next).  A thief issues its
+// candidate scan at frame j's end instead (take_late: one 8-byte sc1 load per lane, 64 slots
+// spread over XCDs and CU slots), picks the candidate with the most unclaimed frames after frame
+// j + 1's forward pass 1 (peek) and issues the steal there; a scan that finds nothing worth
+// stealing ends the workgroup.  (Issued at inverse pass 1 and read at the frame top, the scan's
+// two lane values spilled.)  Only a
+// failed steal (the victim drained meanwhile) waits in next(): up to three synchronous rescans.
+// The slots need no reset between launches: each owner swaps its slot in (one 8-byte atomic) at
+// the start, the swap claiming its first two frames, and a stale slot (the previous launch's, or
+// zero) reads as no frames left.
+constexpr unsigned kStealBias = 0x4000u;
+constexpr int kStealMaxRange = 0x3fff;   // frames per range a word can count (the host checks)
+static_assert(kFsQueueWords >= kFsQueueLineWords + 2 * kFsStealMax, "queue slot: queue lines + steal slots");
+constexpr unsigned STEAL_OOB = 0x80000000u;
+
+__device__ __forceinline__ int steal_front(unsigned x) { return (int)(x >> 16); }
+__device__ __forceinline__ int steal_end(unsigned x) { return (int)(x & 0xffffu) - (int)kStealBias; }
+
+struct StealSchedule {
+    enum { kOwn, kScan, kSteal, kDone, kPriv, kStatic };
+    __amdgpu_buffer_rsrc_t rs;   // the launch's steal slots, [G] x {word, a}
+    int a;          // own range start (absolute frame)
+    int nx, pe;     // the next private frame and the private prefix's end (absolute)
+    int own_left;   // public own frames not yet claimed, as the last claim saw them; -1: stealing
+    int mode;       // what is pending
+    int tk;         // lane 0: the pending atomic's result; every lane: its candidate's word
+    int ta;         // every lane: its candidate's range start (scan)
+    int va;         // the pending steal's victim range start
+    int lim;        // frames of the launch (no claim returns a frame past it)
+    int minrem;     // steal only from ranges with at least this many unclaimed frames
+
+    // this lane's scan candidate of probe k (byte offset of its slot): 64 slots spread over XCDs
+    // (blockIdx % 8) and CU slots (blockIdx / (G / 4)); stride S odd and > G / 64 for G >= 128, so
+    // the 64 are distinct and not w; lanes past G - 1 candidates are out of the buffer (dropped)
+    __device__ __forceinline__ unsigned cand_off(int k) const
+    {
+        const int G = (int)gridDim.x, w = (int)blockIdx.x;
+        const int l = (int)(threadIdx.x & 63);
+        if (l >= G - 1) return STEAL_OOB;
+        const int S = G >= 128 ? (G >> 6) + 1 : 1;
+        int v = w + 1 + (k & 1) + S * l;   // < 3 G
+        v = v >= G ? v - G : v;
+        v = v >= G ? v - G : v;
+        return 8u * (unsigned)v;
+    }
+    __device__ __forceinline__ void claim_own()
+    {
+        const unsigned voff = (threadIdx.x & 63) == 0 ? 8u * blockIdx.x : STEAL_OOB;
+        tk = __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(0x10000, rs, voff, 0, 0);
+        mode = kOwn;
+    }
+    __device__ __forceinline__ void scan(int k)
+    {
+        const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, cand_off(k), 0, 16);   // sc1: the atomics' values
+        tk = (int)v.x;
+        ta = (int)v.y;
+        mode = kScan;
+    }
+    // from the scan in tk / ta: the candidate with the most unclaimed frames; issues the steal
+    // (mode kSteal) or, with none at minrem or more, ends (kDone)
+    __device__ __forceinline__ void choose(int k)
+    {
+        const unsigned off = cand_off(k);
+        const int rem = off != STEAL_OOB ? steal_end((unsigned)tk) - steal_front((unsigned)tk) : -0x7fff;
+        int m = rem;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) m = max(m, __shfl_xor(m, o, 64));
+        m = __builtin_amdgcn_readfirstlane(m);
+        if (m < minrem) {
+            mode = kDone;
+            return;
+        }
+        const int lane = __builtin_ctzll(__builtin_amdgcn_ballot_w64(rem == m));
+        const unsigned voff = __builtin_amdgcn_readlane((int)off, lane);
+        va = __builtin_amdgcn_readlane(ta, lane);
+        tk = __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(-1, rs, (threadIdx.x & 63) == 0 ? voff : STEAL_OOB, 0, 0);
+        mode = kSteal;
+    }
+    // the frame the steal in tk claimed, or -1
+    __device__ __forceinline__ int stolen() const
+    {
+        const unsigned old = (unsigned)__builtin_amdgcn_readfirstlane(tk);
+        const int fr = steal_front(old), er = steal_end(old), f = va + er - 1;
+        return er - 1 >= fr && f < lim ? f : -1;
+    }
+
+    // pub: frames at the end of each range that thieves may take (0: all but the first two);
+    // the owner takes the rest (its private prefix) without atomics.  minrem <= 0: the static
+    // split alone (no atomics at all).
+    __device__ __forceinline__ void init(unsigned *wq, int nframes, int ns, int w, int G, unsigned slotw, int (&f)[1],
+                                         int minrem_, int pub)
+    {
+        unsigned *slots = wq + kFsQueueLineWords;
+        rs = __builtin_amdgcn_make_buffer_rsrc(slots, (short)0, 8 * G, 0x00020000);
+        lim = nframes;
+        minrem = minrem_;
+        a = slot_split(ns, G, w, slotw);
+        const int len = slot_split(ns, G, w + 1, slotw) - a;
+        f[0] = len > 0 ? a : -1;
+        nx = a + 1;
+        if (minrem <= 0) {
+            pe = a + len;
+            mode = kStatic;
+            return;
+        }
+        // the private prefix: at least the first two frames, so that the first atomic claim is
+        // issued a frame after the swap (same lane, same word: in order anyway)
+        const int two = len < 2 ? len : 2;
+        const int P = pub > 0 && len - pub > two ? len - pub : two;
+        pe = a + P;
+        own_left = len - P;
+        mode = kPriv;
+        if ((threadIdx.x & 63) == 0) {
+            const unsigned long long v = ((unsigned long long)(unsigned)a << 32) |
+                                         (((unsigned)P << 16) | (kStealBias + (unsigned)len));
+            (void)atomicExch(reinterpret_cast<unsigned long long *>(slots) + w, v);
+        }
+        if (len <= 0) mode = kDone;   // nothing of its own (a tiny batch)
+        else take_late();             // a one-frame range steals from its first frame on
+    }
+    __device__ __forceinline__ void peek()
+    {
+        if (mode == kScan) choose(0);
+    }
+    __device__ __forceinline__ int next()
+    {
+        if (nx < pe) return nx++;
+        if (mode == kDone || mode == kStatic) return -1;
+        if (mode == kOwn) {
+            const unsigned old = (unsigned)__builtin_amdgcn_readfirstlane(tk);
+            const int fr = steal_front(old), er = steal_end(old);
+            if (fr < er && a + fr < lim) {
+                own_left = er - fr - 1;
+                return a + fr;
+            }
+        } else if (mode == kSteal) {
+            const int f = stolen();
+            if (f >= 0) return f;
+        }
+        // the own claim or the steal failed: steal with waits, up to three probes
+        own_left = -1;
+        for (int k = 1; k <= 3; k++) {
+            scan(k);
+            choose(k);
+            if (mode == kDone) return -1;
+            const int f = stolen();
+            if (f >= 0) return f;
+        }
+        mode = kDone;
+        return -1;
+    }
+    // at inverse pass 1: the own claim for the frame after the next one, past the private prefix
+    __device__ __forceinline__ void take()
+    {
+        if (mode != kDone && mode != kStatic && nx >= pe && own_left > 0) claim_own();
+    }
+    // at the frame's end (the IQ stores issued): a thief's scan, read at the next frame's peek
+    __device__ __forceinline__ void take_late()
+    {
+        if (mode != kDone && mode != kStatic && nx >= pe && own_left <= 0) scan(0), own_left = -1;
     }
 };
 

@@ -232,7 +232,7 @@ struct sddc_ddc {
     unsigned *d_queue = nullptr;
     int queue_slot = 0;
     int slot_weights = sddc::kSlotWeighting;    // the persistent kernel's slot-weighted split (ddc_queue.hpp)
-    int fs_static_pct = sddc::kFsStaticPct;   // the d = 0 kernel's static share of frames (ddc_queue.hpp)
+    sddc::FsSched fs_sched;                    // the d = 0 kernel's frame schedule (ddc_kernels.h)
     hipStream_t q_s[kQueueSlots] = {};
     bool q_used[kQueueSlots] = {};
     bool q_dirty[kQueueSlots] = {};
@@ -720,14 +720,16 @@ static hipError_t launch_single_impl(sddc_ddc_t *h, const int16_t *d_in, int nbl
         } else if (hipError_t e = order_after_build(h, h->fs_s, s); e != hipSuccess) {
             return e;
         }
+        // the default static schedule uses no queue slot; the queue and stealing schedules (A/B)
+        // take one of the ring's slots per launch
         unsigned *wq = nullptr;
-        int qi = 0;
-        hipError_t e = next_queue_slot(h, s, &wq, &qi);
-        if (e != hipSuccess) return e;
+        int qi = -1;
+        hipError_t e = hipSuccess;
+        if (h->fs_sched.sched != 0 && (e = next_queue_slot(h, s, &wq, &qi)) != hipSuccess) return e;
         e = sddc::launch_frames_fs(h->tables, d_in, nblk, d_out, pqf, fsl, h->tunebin, h->lsb, h->rand,
                                    h->out_fmt == SDDC_DDC_FMT_CS16, h->cs16_scale, nco_starts, nco_trig, wq,
-                                   h->fs_static_pct, h->device, s);
-        queue_slot_launched(h, qi, s, e);
+                                   h->fs_sched, h->device, s);
+        if (qi >= 0) queue_slot_launched(h, qi, s, e);
         if (e != hipSuccess) return e;
         return h->readers.record(s);
     }
@@ -812,7 +814,26 @@ int sddc_ddc_internal_set_param(sddc_ddc_t *h, int param, int value)
         return SDDC_OK;
     case SDDC_DDC_PARAM_FS_STATIC_PCT:
         if (value < 0 || value > 100) return fail(SDDC_ERR_ARG, "static share %d outside 0..100", value);
-        h->fs_static_pct = value;
+        h->fs_sched.static_pct = value;
+        return SDDC_OK;
+    case SDDC_DDC_PARAM_FS_FRAMES_PER_WG:
+        if (value < 0 || value > 1024) return fail(SDDC_ERR_ARG, "frames per workgroup %d outside 0..1024", value);
+        h->fs_sched.fpw = value;
+        return SDDC_OK;
+    case SDDC_DDC_PARAM_FS_SCHEDULE:
+        if (value < 0 || value > 2) return fail(SDDC_ERR_ARG, "FS schedule %d outside 0..2", value);
+        h->fs_sched.sched = value;
+        return SDDC_OK;
+    case SDDC_DDC_PARAM_FS_STEAL_MINREM:
+        if (value < 0 || value > 64) return fail(SDDC_ERR_ARG, "steal threshold %d outside 0..64", value);
+        h->fs_sched.minrem = value;
+        return SDDC_OK;
+    case SDDC_DDC_PARAM_FS_ZERO_ROWS:
+        h->fs_sched.zr = value != 0;
+        return SDDC_OK;
+    case SDDC_DDC_PARAM_FS_STEAL_PUBLIC:
+        if (value < 0 || value > 1024) return fail(SDDC_ERR_ARG, "public frames %d outside 0..1024", value);
+        h->fs_sched.pub = value;
         return SDDC_OK;
     default:
         return fail(SDDC_ERR_ARG, "unknown parameter %d", param);

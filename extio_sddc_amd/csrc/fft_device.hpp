@@ -164,6 +164,62 @@ __device__ __forceinline__ void dft16(const float2 *v, float2 *o)
     }
 }
 
+// dft16 with inputs known to be zero: ZR > 0: v[16 - ZR .. 15], ZR < 0: v[0 .. -ZR - 1]
+// (|ZR| = 4 or 8: whole inputs of every first-stage radix-4, n = 4 n1 + n2 with n1 = 3, or n1 = 2, 3,
+// or n1 = 0, or n1 = 0, 1).  Those radix-4s take their sums and differences from the live inputs
+// alone (x + 0 is not folded by the compiler: signed zeros), and the rest is dft16's; the outputs
+// equal dft16's on the same values exactly (the zero terms add nothing).
+template <int DIR, int ZR>
+__device__ __forceinline__ void dft16z(const float2 *v, float2 *o)
+{
+    static_assert(ZR == 0 || ZR == 4 || ZR == -4 || ZR == 8 || ZR == -8, "zero rows: 0, +-4, +-8");
+    if constexpr (ZR == 0) {
+        dft16<DIR>(v, o);
+    } else {
+        constexpr float kT1 = 0.41421356237309504880f;
+        constexpr float kT3 = 2.41421356237309504880f;
+        float2 b[4][4];  // b[n2][k1]
+#pragma unroll
+        for (int n2 = 0; n2 < 4; n2++) {
+            const float2 a0 = v[n2], a1 = v[4 + n2], a2 = v[8 + n2], a3 = v[12 + n2];
+            float2 t0, t1, t2, t3;
+            if constexpr (ZR == 4) {   // a3 = 0
+                t0 = cadd(a0, a2), t1 = csub(a0, a2), t2 = a1, t3 = mulj<DIR>(a1);
+            } else if constexpr (ZR == 8) {   // a2 = a3 = 0
+                t0 = a0, t1 = a0, t2 = a1, t3 = mulj<DIR>(a1);
+            } else if constexpr (ZR == -4) {   // a0 = 0
+                t0 = a2, t1 = make_float2(-a2.x, -a2.y), t2 = cadd(a1, a3), t3 = mulj<DIR>(csub(a1, a3));
+            } else {   // a0 = a1 = 0
+                t0 = a2, t1 = make_float2(-a2.x, -a2.y), t2 = a3, t3 = mulj<DIR>(make_float2(-a3.x, -a3.y));
+            }
+            b[n2][0] = cadd(t0, t2);
+            b[n2][2] = csub(t0, t2);
+            b[n2][1] = cadd(t1, t3);
+            b[n2][3] = csub(t1, t3);
+        }
+        dft4<DIR>(b[0][0], b[1][0], b[2][0], b[3][0], o[0], o[4], o[8], o[12]);
+        float2 t0, t1, p, q;
+        {   // k1 = 1 (as dft16)
+            axpm(b[0][1], kR2, rot1(b[2][1], (float)DIR), t0, t1);
+            axpm(rot1(b[1][1], DIR * kT1), kT1, rot1(b[3][1], DIR * kT3), p, q);
+            axpm(t0, kC16_1, p, o[1], o[9]);
+            ajpm<DIR>(t1, kC16_1, q, o[5], o[13]);
+        }
+        {   // k1 = 2
+            ajpm<DIR>(b[0][2], 1.f, b[2][2], t0, t1);
+            axpm(rot1(b[1][2], (float)DIR), -1.f, rot1(b[3][2], (float)-DIR), p, q);
+            axpm(t0, kR2, p, o[2], o[10]);
+            ajpm<DIR>(t1, kR2, q, o[6], o[14]);
+        }
+        {   // k1 = 3
+            axpm(b[0][3], -kR2, rot1(b[2][3], (float)-DIR), t0, t1);
+            axpm(rot1(b[1][3], DIR * kT3), -kT3, rot1(b[3][3], DIR * kT1), p, q);
+            axpm(t0, kS16_1, p, o[3], o[11]);
+            ajpm<DIR>(t1, kS16_1, q, o[7], o[15]);
+        }
+    }
+}
+
 // dft16 computing only the outputs o[k1 + 4 k2] of the groups k1 = 0, 1 and, when the
 // (wave-uniform) flags ask, k1 = 2, 3: the first stage's k1 = 2, 3 outputs and the whole
 // second-stage group are skipped otherwise (same operations as dft16 for what it computes).

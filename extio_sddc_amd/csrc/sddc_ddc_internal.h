@@ -18,6 +18,23 @@ int sddc_ddc_internal_set_variant(sddc_ddc_t *h, int variant);
 /* SDDC_DDC_PARAM_SLOT_WEIGHTS = 1: the persistent kernel splits the frames by CU slot speed
  * (kSlotWeights[d]), 0: equal contiguous ranges (default kSlotWeighting). */
 #define SDDC_DDC_PARAM_SLOT_WEIGHTS 2
+/* SDDC_DDC_PARAM_FS_FRAMES_PER_WG = n > 0: the d = 0 kernel runs a non-persistent grid of
+ * ceil(frames / n) workgroups, n frames each, balanced by the hardware dispatcher; 0 (default):
+ * the persistent grid. */
+#define SDDC_DDC_PARAM_FS_FRAMES_PER_WG 3
+/* SDDC_DDC_PARAM_FS_SCHEDULE: the d = 0 kernel's frame schedule, 0 = the slot-weighted static
+ * split alone (default), 1 = static prefix + dynamic queue, 2 = work stealing (1 and 2 only for
+ * CF32 output without NCO, rand or sideband inversion; other configurations fail to launch). */
+#define SDDC_DDC_PARAM_FS_SCHEDULE 4
+/* SDDC_DDC_PARAM_FS_STEAL_MINREM: a thief steals only from ranges with at least this many
+ * unclaimed frames (1..64; 0: no stealing, the static split inside the stealing kernel). */
+#define SDDC_DDC_PARAM_FS_STEAL_MINREM 5
+/* SDDC_DDC_PARAM_FS_STEAL_PUBLIC: frames at the end of each workgroup's range open to thieves,
+ * claimed by the owner with atomics (0: all but the first two); the rest the owner takes alone. */
+#define SDDC_DDC_PARAM_FS_STEAL_PUBLIC 6
+/* SDDC_DDC_PARAM_FS_ZERO_ROWS = 1 (default): the d = 0 kernel skips the inverse input's whole zero
+ * rows of the tune bin (4 rows when tb <= 1024 or tb >= 3072); 0: computes them (A/B). */
+#define SDDC_DDC_PARAM_FS_ZERO_ROWS 7
 
 int sddc_ddc_internal_set_param(sddc_ddc_t *h, int param, int value);
 /* Diagnostic stamp buffers of -DSDDC_STAMPS builds (tools/fs_stamps.py); -1 in product builds. */

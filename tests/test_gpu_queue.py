@@ -63,12 +63,12 @@ def device_stream(torch, nblk, seed):
     return torch.cat([torch.zeros(HIST, dtype=torch.int16, device="cuda"), x])
 
 
-def run(torch, ddc, d_in, nblk, d, tb, stream=None):
+def run(torch, ddc, d_in, nblk, d, tb, stream=None, lsb=0, rand=0):
     from extio_sddc_amd import output_samples
     ddc.setDecimate(d)
     ddc.setTuneBin(tb)
-    ddc.setSideband(False)
-    ddc.updateRand(False)
+    ddc.setSideband(bool(lsb))
+    ddc.updateRand(bool(rand))
     d_out = torch.full((output_samples(d, nblk) * 2,), float("nan"), dtype=torch.float32, device="cuda")
     torch.cuda.synchronize()
     ddc.process_device(d_in, nblk, d_out, stream=stream)
@@ -91,12 +91,31 @@ def shard_windows(nblk, extra_seed):
     return sorted(starts)
 
 
-def check_windows(oracle, H, x, y, nblk, d, tb, starts):
+# CU-slot weights of the slot-weighted split (ddc_kernels.h kFsSlotWeights / kSlotWeights)
+SLOT_WEIGHTS = {0: (31, 26, 18, 13), 1: (31, 26, 18, 13), 2: (31, 26, 18, 13), 3: (29, 25, 20, 15),
+                4: (29, 25, 20, 15), 5: (29, 25, 20, 15), 6: (29, 25, 20, 15)}
+
+
+def quarter_windows(nblk, d):
+    """Start blocks of 2-block windows at the first, middle and last frame of each workgroup
+    quarter's share of a full-residency launch (ddc_queue.hpp slot_split: quarter q takes the
+    frames [ns W_q / W, ns W_{q+1} / W) with W_q the cumulative slot weight)."""
+    nframes = FRAMES * nblk
+    w = np.cumsum((0,) + SLOT_WEIGHTS[d])
+    starts = set()
+    for q in range(4):
+        lo, hi = nframes * w[q] // w[4], nframes * w[q + 1] // w[4]
+        for f in (lo, (lo + hi) // 2, hi - 1):
+            starts.add(min(max(f // FRAMES - (1 if f % FRAMES == 0 else 0), 0), nblk - 2))
+    return sorted(starts)
+
+
+def check_windows(oracle, H, x, y, nblk, d, tb, starts, lsb=0, rand=0):
     per = 32768 >> d
     worst = 0.0
     for b in starts:
         seg = x[BLOCK * b: HIST + BLOCK * (b + 2)]   # the window's real history + 2 blocks
-        r = oracle.r2iq(seg, 2, d, tb, H=H)
+        r = oracle.r2iq(seg, 2, d, tb, lsb, rand, H=H)
         yw = y[b * per:(b + 2) * per]
         err = oracle.max_rel_err(yw, r)
         worst = max(worst, err)
@@ -142,27 +161,43 @@ def test_queue_path_headline_every_block(torch_dev, ddc, oracle, H):
     assert num / den <= TOL, f"max-rel-err {num / den:.3e}"
 
 
-@pytest.mark.parametrize("d", [1, 2, 4])
-def test_queue_path_shard_windows_2048(torch_dev, ddc, oracle, H, d):
-    """2048 blocks at d = 1, 2 (queue with two static frames per workgroup) and d = 4 (static
-    contiguous split): 2-block windows from every shard, the last block and random blocks."""
+@pytest.mark.parametrize("d,lsb,rand", [(1, 0, 0), (2, 0, 0), (4, 0, 0),
+                                        (1, 1, 1),   # C4: decim 4, sideband inversion + rand (RAND/LSB instances)
+                                        (3, 0, 0),   # C3 decim 16
+                                        (5, 0, 0), (6, 0, 0),
+                                        (0, 1, 1)])  # the FS kernel's RAND/LSB instance
+def test_headline_size_windows_2048(torch_dev, ddc, oracle, H, d, lsb, rand):
+    """2048-block launches (every workgroup carries ~22 frames: input prefetch, LDS reuse across
+    frames, the slot-weighted ranges) into NaN-filled outputs: 2-block windows at the first,
+    middle and last frame of every workgroup quarter's share and of 8 equal stretches, the last
+    block and random blocks, each with its real history, against the f64 oracle at 1e-5
+    (fft_mt_r2iq_impl.hpp:76-138)."""
     torch = torch_dev
     nblk, tb = 2048, 1024
-    d_in = device_stream(torch, nblk, 0x5DDC + 16 * d)
-    d_out = run(torch, ddc, d_in, nblk, d, tb)
+    d_in = device_stream(torch, nblk, 0x5DDC + 16 * d + 4 * lsb + 2 * rand)
+    d_out = run(torch, ddc, d_in, nblk, d, tb, lsb=lsb, rand=rand)
     assert bool(torch.isfinite(d_out).all()), "frames left unwritten"
     y = d_out.cpu().numpy().view(np.complex64)
+    del d_out
     x = d_in.cpu().numpy()
-    check_windows(oracle, H, x, y, nblk, d, tb, shard_windows(nblk, d))
+    del d_in
+    starts = sorted(set(shard_windows(nblk, d)) | set(quarter_windows(nblk, d)))
+    check_windows(oracle, H, x, y, nblk, d, tb, starts, lsb, rand)
 
 
-@pytest.mark.parametrize("d", [0, 1])
-def test_queue_ring_reuse_across_streams(torch_dev, ddc, d):
+@pytest.mark.parametrize("d,sched", [(0, 1), (0, 2), (0, 0), (1, 0)])
+def test_queue_ring_reuse_across_streams(torch_dev, d, sched):
     """More launches than queue slots (72 > 64), round-robin over three streams, the first one
     backed up behind a 2048-block launch, each into its own NaN-filled output: every output
-    equals the same launch run alone on one stream, bit for bit (no frame dropped or doubled)."""
+    equals the same launch run alone on one stream, bit for bit (no frame dropped or doubled).
+    sched: the FS kernel's schedule (1 the queue and 2 work stealing take a ring slot per launch;
+    0, the default static split, and the persistent kernel at d = 1 take none)."""
     torch = torch_dev
-    from extio_sddc_amd import output_samples
+    from extio_sddc_amd import R2iq, output_samples
+    ddc = R2iq(gain=1.0, device=0)
+    _set_param(ddc, P_FS_SCHEDULE, sched)
+    if sched == 1:
+        _set_param(ddc, P_FS_STATIC_PCT, 40)
     nblk, nlaunch, noff = 48, 72, 8
     d_in = device_stream(torch, 2048, 0x5DDC + 100 + d)
     ddc.setDecimate(d)
@@ -192,6 +227,7 @@ def test_queue_ring_reuse_across_streams(torch_dev, ddc, d):
     ddc.process_device(d_in, nblk, again)
     torch.cuda.synchronize()
     assert torch.equal(again, refs[0])
+    ddc.close()
 
 
 @pytest.mark.parametrize("d,tb0,tb1", [(0, 1024, 2048), (1, 1024, 2048)])
@@ -226,7 +262,8 @@ def test_table_rebuild_seen_by_other_stream(torch_dev, ddc, oracle, H, d, tb0, t
     assert torch.equal(ya, yb)
 
 
-P_FS_STATIC_PCT, P_SLOT_WEIGHTS = 1, 2   # sddc_ddc_internal.h SDDC_DDC_PARAM_*
+# sddc_ddc_internal.h SDDC_DDC_PARAM_*
+P_FS_STATIC_PCT, P_SLOT_WEIGHTS, P_FS_SCHEDULE, P_FS_MINREM, P_FS_PUBLIC, P_FS_ZERO_ROWS = 1, 2, 4, 5, 6, 7
 
 
 def _set_param(r, param, value):
@@ -238,26 +275,86 @@ def _set_param(r, param, value):
     _lib.check(f(r._h, param, value))
 
 
-@pytest.mark.parametrize("d,param,values", [(0, P_FS_STATIC_PCT, (100, 40, 0)), (1, P_SLOT_WEIGHTS, (1, 0)),
-                                            (4, P_SLOT_WEIGHTS, (1, 0))])
-def test_schedules_bit_identical(torch_dev, d, param, values):
-    """the FS queue at static shares 40 % and 0 % (every frame from the queue), and the equal
-    split instead of the slot-weighted one, against the default, 2048 blocks, NaN-filled"""
+SCHEDULES = {
+    # d = 0 (FS kernel): the static split (default), the queue at static shares 100 / 40 / 0 %,
+    # work stealing (every frame open / the last 4 of each range, steal threshold 2 / disabled),
+    # and the zero rows computed instead of skipped
+    0: [(), ((P_FS_SCHEDULE, 1), (P_FS_STATIC_PCT, 100)), ((P_FS_SCHEDULE, 1), (P_FS_STATIC_PCT, 40)),
+        ((P_FS_SCHEDULE, 1), (P_FS_STATIC_PCT, 0)), ((P_FS_SCHEDULE, 2),),
+        ((P_FS_SCHEDULE, 2), (P_FS_PUBLIC, 4), (P_FS_MINREM, 2)), ((P_FS_SCHEDULE, 2), (P_FS_MINREM, 0)),
+        ((P_FS_ZERO_ROWS, 0),)],
+    # persistent kernel: slot-weighted vs equal contiguous split
+    1: [(), ((P_SLOT_WEIGHTS, 0),)],
+    4: [(), ((P_SLOT_WEIGHTS, 0),)],
+}
+
+
+@pytest.mark.parametrize("d", [0, 1, 4])
+def test_schedules_bit_identical(torch_dev, d):
+    """Every schedule computes each frame the same way: the FS kernel's queue (static shares
+    100 / 40 / 0 %), work stealing in its forms, the zero rows computed, and the equal split
+    instead of the slot-weighted one, each against the default, 2048 blocks, NaN-filled"""
     torch = torch_dev
     from extio_sddc_amd import R2iq, output_samples
     nblk = 2048
     g = torch.Generator(device="cuda").manual_seed(0x5DDC + d)
     d_in = torch.randint(-32768, 32767, (HIST + nblk * BLOCK,), dtype=torch.int16, device="cuda", generator=g)
     outs = []
-    with R2iq(gain=1.0, device=0) as r:
-        r.setDecimate(d)
-        r.setTuneBin(1024)
-        for v in values:
-            _set_param(r, param, v)
+    for settings in SCHEDULES[d]:
+        with R2iq(gain=1.0, device=0) as r:
+            r.setDecimate(d)
+            r.setTuneBin(1024)
+            for param, v in settings:
+                _set_param(r, param, v)
             out = torch.full((output_samples(d, nblk) * 2,), float("nan"), dtype=torch.float32, device="cuda")
             r.process_device(d_in, nblk, out)
             torch.cuda.synchronize()
             outs.append(out.view(torch.int32).cpu().numpy())
     assert not np.any(np.isnan(outs[0].view(np.float32))), "frames left unwritten"
-    for o in outs[1:]:
-        np.testing.assert_array_equal(o, outs[0])
+    for o, settings in zip(outs[1:], SCHEDULES[d][1:]):
+        assert not np.any(np.isnan(o.view(np.float32))), f"{settings}: frames left unwritten"
+        np.testing.assert_array_equal(o, outs[0], err_msg=str(settings))
+
+
+# d = 0 tune bins by the inverse input's whole zero rows (the reference's zero fill,
+# impl.hpp:91-96): (tb, rows zero at the top (bins >= tb + 2048), rows zero at the bottom
+# (bins < tb - 2048)); the FS kernel skips 4 of them when there are 4 or more (ZR = +-4)
+ZERO_ROW_BINS = [(2048, 0, 0), (1792, 1, 0), (1028, 3, 0), (1024, 4, 0), (256, 7, 0), (0, 8, 0),
+                 (2304, 0, 1), (3068, 0, 3), (3072, 0, 4), (3840, 0, 7), (4092, 0, 7)]
+
+
+@pytest.mark.parametrize("tb,ztop,zbot", ZERO_ROW_BINS)
+def test_fs_zero_rows(torch_dev, oracle, H, tb, ztop, zbot):
+    """The zero-row skip at tune bins giving 0, 1, 3, 4, 7 and 8 zero rows (top and bottom):
+    within 1e-5 of the f64 oracle (4 blocks, strong out-of-band + weak in-band tone and a mix),
+    and equal to the same launch with the zero rows computed (64 blocks, NaN-filled)"""
+    torch = torch_dev
+    from extio_sddc_amd import R2iq, output_samples
+    from extio_sddc_amd.synth import make_stream
+    assert (2048 - tb) // 256 == ztop if tb <= 2048 else (tb - 2048) // 256 == zbot
+    for src in ("mix", "oob"):
+        x = make_stream(4, src)
+        with R2iq(gain=1.0, device=0) as r:
+            r.setDecimate(0)
+            r.setTuneBin(tb)
+            d_in = torch.from_numpy(x).to("cuda")
+            out = torch.full((output_samples(0, 4) * 2,), float("nan"), dtype=torch.float32, device="cuda")
+            r.process_device(d_in, 4, out)
+            torch.cuda.synchronize()
+        y = out.cpu().numpy().view(np.complex64)
+        err = oracle.max_rel_err(y, oracle.r2iq(x, 4, 0, tb, H=H))
+        assert err <= TOL, f"{src}: max-rel-err {err:.3e}"
+    nblk = 64
+    d_in = device_stream(torch, nblk, 0x5DDC + tb)
+    outs = []
+    for zr in (1, 0):
+        with R2iq(gain=1.0, device=0) as r:
+            r.setDecimate(0)
+            r.setTuneBin(tb)
+            _set_param(r, P_FS_ZERO_ROWS, zr)
+            out = torch.full((output_samples(0, nblk) * 2,), float("nan"), dtype=torch.float32, device="cuda")
+            r.process_device(d_in, nblk, out)
+            torch.cuda.synchronize()
+            outs.append(out.cpu().numpy())
+    assert np.all(np.isfinite(outs[0]))
+    np.testing.assert_array_equal(outs[0], outs[1])

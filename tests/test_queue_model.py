@@ -190,3 +190,164 @@ def test_slot_split_partitions_the_frames(nframes, G, slotw):
         w = [(slotw >> (8 * k)) & 0xFF for k in range(4)]
         for q in range(4):
             assert abs(per[q] / nframes - w[q] / sum(w)) < 1e-3
+
+
+# ---------------------------------------------------------------------------------------------
+# Work stealing (ddc_queue.hpp StealSchedule, the FS kernel's A/B schedule since round 5): per
+# workgroup one word (front << 16) | (BIAS + end) over its slot-weighted range; the owner claims
+# with add(0x10000) past its private prefix, thieves steal the range's last frame with add(-1).
+# The model keeps the kernel's pipelining: the owner's claim for frame j + 2 is issued at frame j
+# (take) and read at frame j + 1 (next); a thief's scan is issued at the end of a frame, the steal
+# atomic at the next frame's peek and read at its next(); a failed steal rescans (up to 3 probes).
+# Every atomic and every scan load is a yield point, so the random scheduler interleaves them.
+# ---------------------------------------------------------------------------------------------
+BIAS = 0x4000
+
+
+class StealWords:
+    def __init__(self, grid):
+        self.w = [0] * grid      # zero slots: "no frames left" (a fresh or dirty ring slot)
+        self.a = [0] * grid
+
+    def add(self, v, x):
+        old = self.w[v]
+        self.w[v] = (old + x) & 0xFFFFFFFF
+        return old
+
+
+def steal_front(x):
+    return x >> 16
+
+
+def steal_end(x):
+    return (x & 0xFFFF) - BIAS
+
+
+def steal_workgroup(w, nframes, grid, slotw, pub, minrem, words, out, rng):
+    a = slot_split(nframes, grid, w, slotw)
+    b = slot_split(nframes, grid, w + 1, slotw)
+    length = b - a
+    two = min(length, 2)
+    P = length - pub if pub > 0 and length - pub > two else two
+    S = (grid >> 6) + 1 if grid >= 128 else 1
+
+    def cands(k):
+        res = []
+        for lane in range(64):
+            if lane >= grid - 1:
+                continue
+            v = w + 1 + (k & 1) + S * lane
+            v = v - grid if v >= grid else v
+            v = v - grid if v >= grid else v
+            res.append(v)
+        return res
+
+    yield   # the swap
+    words.w[w] = (P << 16) | (BIAS + length)
+    words.a[w] = a
+    st = {"mode": "priv", "nx": a + 1, "pe": a + P, "own_left": length - P, "tk": None, "scan": None, "va": 0}
+    frames = [a] if length > 0 else []
+    if length <= 0:
+        st["mode"] = "done"
+
+    def scan(k):
+        snap = [(v, words.w[v], words.a[v]) for v in cands(k)]   # sc1 loads (one snapshot per probe)
+        st["scan"] = (k, snap)
+        st["mode"] = "scan"
+
+    def choose():
+        k, snap = st["scan"]
+        rems = [(steal_end(x) - steal_front(x), v, av) for v, x, av in snap]
+        if not rems:
+            st["mode"] = "done"
+            return False
+        m = max(r for r, _, _ in rems)
+        if m < minrem:
+            st["mode"] = "done"
+            return False
+        _, v, av = next(t for t in rems if t[0] == m)
+        st["victim"], st["va"], st["mode"] = v, av, "steal"
+        return True
+
+    def stolen(old):
+        fr, er = steal_front(old), steal_end(old)
+        f = st["va"] + er - 1
+        return f if er - 1 >= fr and f < nframes else -1
+
+    def take_late():
+        if st["mode"] not in ("done",) and st["nx"] >= st["pe"] and st["own_left"] <= 0:
+            st["own_left"] = -1
+            scan(0)
+
+    if length == 1:
+        take_late()
+        yield
+    while frames:
+        f = frames.pop()
+        out.append(f)
+        # peek (after the frame's forward pass 1): a pending scan becomes a steal
+        if st["mode"] == "scan":
+            if choose():
+                yield
+                st["tk"] = words.add(st["victim"], -1)
+        # next (inverse pass 0): the frame after this one
+        fn = -1
+        if st["nx"] < st["pe"]:
+            fn = st["nx"]
+            st["nx"] += 1
+        elif st["mode"] == "own":
+            old = st["tk"]
+            fr, er = steal_front(old), steal_end(old)
+            if fr < er and a + fr < nframes:
+                st["own_left"] = er - fr - 1
+                fn = a + fr
+        elif st["mode"] == "steal":
+            fn = stolen(st["tk"])
+        if fn < 0 and st["mode"] in ("own", "steal"):
+            st["own_left"] = -1
+            for k in (1, 2, 3):
+                yield
+                scan(k)
+                if not choose():
+                    break
+                yield
+                fn = stolen(words.add(st["victim"], -1))
+                if fn >= 0:
+                    break
+            if fn < 0:
+                st["mode"] = "done"
+        if fn < 0:
+            break
+        frames.append(fn)
+        # take (inverse pass 1): the own claim for the frame after fn
+        if st["mode"] != "done" and st["nx"] >= st["pe"] and st["own_left"] > 0:
+            yield
+            st["tk"] = words.add(w, 0x10000)
+            st["mode"] = "own"
+        # frame end: a thief's scan
+        yield
+        take_late()
+
+
+@pytest.mark.parametrize("nframes,grid,slotw,pub,minrem", [
+    (11 * 256, 1024, W_FS, 0, 1), (11 * 256, 1024, W_FS, 4, 2), (11 * 64, 128, W_FS, 0, 1),
+    (37, 36, 0, 0, 1), (11 * 3, 8, 0, 2, 1), (11 * 40, 64, W_FS, 3, 1), (500, 96, W_FS, 0, 2)])
+def test_steal_every_frame_once(nframes, grid, slotw, pub, minrem):
+    for seed in range(4):
+        rng = random.Random(seed * 7919 + nframes)
+        words = StealWords(grid)
+        outs = [[] for _ in range(grid)]
+        gens = [steal_workgroup(w, nframes, grid, slotw, pub, minrem, words, outs[w], rng) for w in range(grid)]
+        live = list(range(grid))
+        while live:
+            i = rng.randrange(len(live))
+            try:
+                next(gens[live[i]])
+            except StopIteration:
+                live.pop(i)
+        done = sorted(f for o in outs for f in o)
+        assert done == list(range(nframes)), f"seed {seed}: frames missing or doubled"
+        stolen = sum(1 for w in range(grid) for f in outs[w]
+                     if not slot_split(nframes, grid, w, slotw) <= f < slot_split(nframes, grid, w + 1, slotw))
+        if seed == 0:
+            print(f"{nframes} frames, {grid} workgroups: {stolen} stolen")

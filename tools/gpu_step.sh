@@ -1,7 +1,8 @@
 #!/bin/bash
 # One GPU-box session of steps, each under its own time limit, stopping at the first crash-like
 # exit (124/134/137/139): GPU tests (optional), an interleaved A/B of libraries, a bench line.
-#   tools/gpu_step.sh TAG [--tests] [--ab "ab_libs args"] [--bench] [--prof]
+#   tools/gpu_step.sh TAG [--tests] [--testsel FILES] [--ab "ab_libs args"] [--stamps "fs_stamps args"]
+#                         [--bench] [--prof]   (options repeat; run in the order given)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"
@@ -19,6 +20,9 @@ while [ $# -gt 0 ]; do
     --ab)
       timeout -k 10 600 python -u tools/ab_libs.py $2 > $O/ab.log 2>&1
       rc=$?; echo "ab rc=$rc" >> $O/ab.log; crashed $rc && exit $rc; shift ;;
+    --stamps)
+      timeout -k 10 300 python -u tools/fs_stamps.py $2 >> $O/stamps.log 2>&1
+      rc=$?; echo "stamps rc=$rc" >> $O/stamps.log; crashed $rc && exit $rc; shift ;;
     --bench)
       timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.log 2>&1
       rc=$?; echo "bench rc=$rc" >> $O/bench.log; crashed $rc && exit $rc ;;
