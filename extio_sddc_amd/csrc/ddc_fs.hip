@@ -203,9 +203,7 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
         asm volatile("" : "+s"(z));
         const int t = tid + z;
         const int c = col_ + z;
-        const int sT = swz(t);
         const int x15 = t & 15;
-        const unsigned xa1 = 2048u * (unsigned)(t >> 4) + 8u * (unsigned)x15;   // st_row base of the F1 / I1 rows
         const int oblk = blk * 8 * HALF;
         const int kc = k;
         // ---- F0 (R16, NS1): convert + DFT16 from registers ----
@@ -224,7 +222,8 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
                 }
             dft16<-1>(a, v);
         }
-        ST_SYNC(0);   // the previous frame's last LDS reads are done
+        // no barrier: this thread's row 17 t .. 17 t + 15 is exactly what it read in the previous
+        // frame's inverse pass 2 (every exchange writes in place of its own reads)
         {
             float2 *const row = lds + 17 * t;
 #pragma unroll
@@ -240,9 +239,13 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
             table_twiddle<-1, true>(a, twl, 16, x15);
             dft16<-1>(a, v);
         }
-        ST_SYNC(2);
+        {
+            // in place of the reads (no barrier): element 256 (t >> 4) + 16 r + x15 at
+            // t + (t >> 4) + 272 r, ds_write_b64 groups of 16 lanes conflict-free
+            float2 *const col = lds + t + (t >> 4);
 #pragma unroll
-        for (int r = 0; r < 16; r++) st_row(lds, xa1, r, 16, v[r]);   // element 256 (t >> 4) + 16 r + (x15 ^ r)
+            for (int r = 0; r < 16; r++) col[272 * r] = v[r];
+        }
         ST_SYNC(3);
         if constexpr (SCHED == kSchedSteal)
             if (qw) fsch.peek();
@@ -259,9 +262,11 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
         asm volatile("" ::: "memory");
         {
             float2 a[16];
-            const int sC = swz(c);
+            // element c + 256 g (F1 thread 16 g + (c & 15), its output c >> 4) at
+            // 272 (c >> 4) + (c & 15) + 17 g: base + immediate; banks c mod 32 (kFsPerm)
+            const float2 *const cb = lds + 272 * (c >> 4) + (c & 15);
 #pragma unroll
-            for (int r = 0; r < 16; r++) XRD(a[r], lds[sC + NT * r]);
+            for (int r = 0; r < 16; r++) XRD(a[r], cb[17 * r]);
             const float2 fw1 = wtab[c], fw4 = wtab[NT + c];   // W^c, W^{4c}
             twiddle_rec16<-1>(a, fw1, fw4);
             dft16<-1>(a, v);
@@ -319,13 +324,15 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
             }
             dft16z<+1, ZR>(a, u);
         }
-        ST_SYNC(4);   // every wave's F2 reads are done
         {
-            // row 16 c + (r ^ (swz(c) & 15)): the key XORs in c >> 4 so that the lane pairs c, -c
-            // (equal c mod 16 for c = 0, 8 mod 16) never share a bank (tools/fs_perm.py)
-            const unsigned xc0 = 128u * (unsigned)c + 8u * (unsigned)(swz(c) & 15);
+            // in place of this thread's F2 reads (no barrier): output r at 272 (c >> 4) + (c & 15)
+            // + 17 r; banks c mod 16 per 16 lanes, the pairs c, -c with c = 0 mod 8 sharing one
+            // (a 2-way conflict inside a ds_write_b64 group costs no time: its transfer is longer)
+            int c1 = c;
+            asm volatile("" : "+v"(c1));
+            float2 *const cb = lds + 272 * (c1 >> 4) + (c1 & 15);
 #pragma unroll
-            for (int r = 0; r < 16; r++) st_row(lds, xc0, r, 0, u[r]);
+            for (int r = 0; r < 16; r++) cb[17 * r] = u[r];
         }
         // the next frame (static, or the ticket read at this frame's top; ddc_queue.hpp)
         if (qw) {
@@ -342,12 +349,11 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
         // ---- I1 (R16, NS16): table twiddles W_256^{-(t%16) r} ----
         {
             float2 a[16];
-            // element j + 256 r was stored by I0 column (j >> 4) + 16 r under the key
-            // swz(column) & 15 = (j >> 4) ^ r: byte (8 sT ^ 8 r) + 2048 r, one v_xor per read
-            const unsigned sT8 = 8u * (unsigned)sT;
+            // element t + 256 r was stored by I0 column (t >> 4) + 16 r (its output t & 15) at
+            // 272 r + (t >> 4) + 17 (t & 15): base + immediate, one 2-way bank conflict per 32 lanes
+            const float2 *const ib = lds + (t >> 4) + 17 * x15;
 #pragma unroll
-            for (int r = 0; r < 16; r++)
-                XRD(a[r], *reinterpret_cast<const float2 *>(reinterpret_cast<const char *>(lds) + ((sT8 ^ (8u * r)) + 2048u * r)));
+            for (int r = 0; r < 16; r++) XRD(a[r], ib[272 * r]);
             // the next frame's number is read behind the data reads (its LDS round trip under
             // theirs), and its input loads are issued here rather than in F0, so their 16
             // registers are free through F2 and the split
@@ -364,22 +370,24 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
             table_twiddle<+1, true>(a, twl, 16, x15);
             dft16<+1>(a, u);
         }
-        ST_SYNC(6);
         {
-            // the same addresses as the F1 stores: recomputed from an opaque copy of t, or the
-            // compiler keeps them live through F2 and spills
+            // in place of this thread's I1 reads (no barrier), recomputed from an opaque copy of
+            // t (else kept live through the pass): element 256 (t >> 4) + 16 r + (t & 15)
             int t1 = t;
             asm volatile("" : "+v"(t1));
-            const unsigned xb1 = 2048u * (unsigned)(t1 >> 4) + 8u * (unsigned)(t1 & 15);
+            float2 *const ib = lds + (t1 >> 4) + 17 * (t1 & 15);
 #pragma unroll
-            for (int r = 0; r < 16; r++) st_row(lds, xb1, r, 16, u[r]);
+            for (int r = 0; r < 16; r++) ib[272 * r] = u[r];
         }
         ST_SYNC(7);
         // ---- I2 (R16, NS256): twiddles g_t W^{-t r}, quarter turns, overlap-discard ----
         {
             float2 a[16];
+            // element t + 256 r (I1 thread 16 r + (t & 15), its output t >> 4) at 17 t + r: the
+            // next frame's F0 row of this thread, conflict-free
+            const float2 *const rb = lds + 17 * t;
 #pragma unroll
-            for (int r = 0; r < 16; r++) XRD(a[r], lds[sT + NT * r]);
+            for (int r = 0; r < 16; r++) XRD(a[r], rb[r]);
             const float2 rw1 = wtab[t], rw4 = wtab[NT + t];   // W^t, W^{4t}
             twiddle_g16<+1>(a, g0, g1, g4, rw1, rw4);
             dft16<+1>(a, u);

@@ -249,6 +249,10 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
     const int zr = ZROT ? (tunebin >> 8) + (tid < zd ? 1 : 0) : r0;
     const float2 fw1_ = tw4096[(tid + 256 * zr) & (HALF - 1)];   // rotated bases (PRUNE: r0, ZROT: zr)
     const float2 fw4_ = tw4096[(4 * tid + 1024 * zr) & (HALF - 1)];
+    // forward pass 2's other anchors W^{2b}, W^{3b}, W^{8b}, W^{12b} (twiddle_anchor6)
+    const int fb_ = tid + 256 * zr;
+    const float2 fw2_ = tw4096[(2 * fb_) & (HALF - 1)], fw3_ = tw4096[(3 * fb_) & (HALF - 1)];
+    const float2 fw8_ = tw4096[(8 * fb_) & (HALF - 1)], fw12_ = tw4096[(12 * fb_) & (HALF - 1)];
     float2 iw1_ = ZROT ? rec_f[tid] : fw1_, iw4_ = ZROT ? rec_f[NT + tid] : fw4_;
     if constexpr (N >= 512 && N < HALF) {
         if (tid < N / 16) {
@@ -288,6 +292,8 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
         const float4 *pqz = pq + z;
         float2 fw1 = fw1_, fw4 = fw4_, iw1 = iw1_, iw4 = iw4_;
         asm volatile("" : "+v"(fw1), "+v"(fw4), "+v"(iw1), "+v"(iw4));
+        float2 fw2 = fw2_, fw3 = fw3_, fw8 = fw8_, fw12 = fw12_;
+        asm volatile("" : "+v"(fw2), "+v"(fw3), "+v"(fw8), "+v"(fw12));
         const int sT = swz(t);            // swz(t + 256 r) = sT + 256 r
         const int x15 = t & 15;
         // row-store bases (st_row): 16 t + (r ^ x15) and 256 (t >> 4) + 16 r + (r ^ x15)
@@ -348,7 +354,7 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
             float2 a[16];
 #pragma unroll
             for (int r = 0; r < 16; r++) XRD(a[r], w1[sT + NT * r]);
-            twiddle_rec16<-1>(a, fw1, fw4);
+            twiddle_anchor6<-1>(a, fw1, fw2, fw3, fw4, fw8, fw12);
             if constexpr (GRP) dft16_groups<-1>(a, v, need2, need3);
             else dft16<-1>(a, v);
         }

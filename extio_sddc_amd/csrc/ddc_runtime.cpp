@@ -637,12 +637,17 @@ static hipError_t next_queue_slot(sddc_ddc_t *h, hipStream_t s, unsigned **wq, i
 }
 
 // after the launch that took slot i: on success the slot's last user is s (the launch is recorded
-// in readers right after); on failure the slot is zeroed before its next use
+// in readers right after); on failure the slot is zeroed before its next use, on a stream ordered
+// after an event recorded on s here: hipGetLastError may report a sticky or earlier error for a
+// kernel that was enqueued and still runs (readers.record of the success path is skipped then)
 static void queue_slot_launched(sddc_ddc_t *h, int i, hipStream_t s, hipError_t e)
 {
     h->q_s[i] = s;
     h->q_used[i] = true;
-    if (e != hipSuccess) h->q_dirty[i] = true;
+    if (e != hipSuccess) {
+        h->q_dirty[i] = true;
+        (void)h->readers.record(s);
+    }
 }
 
 // a HIP error on a launch path: the state of every in-flight launch is unknown, so every queue

@@ -314,6 +314,34 @@ __device__ __forceinline__ void twiddle_rec16(float2 *a, float2 w1, float2 w4)
     a[15] = cmul(a[15], w15);
 }
 
+// a[r] *= W^r for r = 1..15 (forward, DIR = -1) from six exactly rounded anchors W^1, W^2, W^3,
+// W^4, W^8, W^12 of the lane's base: W^{4h + l} = W^{4h} W^l, one product per other power (36
+// VALU, as twiddle_rec16's 38).  More accurate than the recurrence: in the float32 model of the
+// kernel (tools/fp32_model.py, twmode "anchor6") the leakage-only draws of tests/test_gpu_floor.py
+// go from a geometric mean of 0.95 (max 1.68) x the reference-class float32 port's error to 0.81
+// (max 1.17), where the exactly rounded table of all 15 powers gives 0.87 (max 1.44).
+template <int DIR>
+__device__ __forceinline__ void twiddle_anchor6(float2 *a, float2 w1, float2 w2, float2 w3, float2 w4, float2 w8,
+                                                float2 w12)
+{
+    static_assert(DIR < 0, "forward twiddles");
+    a[1] = cmul(a[1], w1);
+    a[2] = cmul(a[2], w2);
+    a[3] = cmul(a[3], w3);
+    a[4] = cmul(a[4], w4);
+    a[5] = cmul(a[5], cmul(w4, w1));
+    a[6] = cmul(a[6], cmul(w4, w2));
+    a[7] = cmul(a[7], cmul(w4, w3));
+    a[8] = cmul(a[8], w8);
+    a[9] = cmul(a[9], cmul(w8, w1));
+    a[10] = cmul(a[10], cmul(w8, w2));
+    a[11] = cmul(a[11], cmul(w8, w3));
+    a[12] = cmul(a[12], w12);
+    a[13] = cmul(a[13], cmul(w12, w1));
+    a[14] = cmul(a[14], cmul(w12, w2));
+    a[15] = cmul(a[15], cmul(w12, w3));
+}
+
 // a[r] *= g W^{r} for r = 0..15 (W conjugated for DIR = +1), with g W^0 = u0, g W^1 = u1 and
 // g W^4 = u4 given (exactly rounded, from the table) and the lane's forward W^1, W^4 for the
 // steps: the same products and Chebyshev steps as twiddle_rec16 on the sequence g W^r (the

@@ -21,7 +21,71 @@ def test_perm_header_is_a_lane_paired_permutation():
     cols = P.read_header()
     assert P.valid(cols)
     wr, rd = P.conflicts(cols)
-    assert (wr, rd) == (0, 0)   # inverse pass-0 stores and forward pass-2 reads conflict-free
+    # the in-place layout's floor: one conflict per lane group, from the pairs c = -c
+    assert (wr, rd) == P.BEST["inplace"]
+
+
+# The in-place LDS layout of the FS kernel (round 5): every exchange's writer stores into exactly
+# the slots it read in the previous exchange, so only the four read-after-write barriers remain.
+# (thread, register) -> (element, slot) of each store and load, as in ddc_fs.hip.
+def _layout(perm):
+    t = np.arange(256)[:, None]
+    r = np.arange(16)[None, :]
+    c = np.asarray(perm)[:, None]
+    cb = 272 * (c >> 4) + (c & 15)
+    ib = (t >> 4) + 17 * (t & 15)
+    return [
+        # (name, store element, store slot, load element, load slot)
+        ("F0->F1", 16 * t + r, 17 * t + r, t + 256 * r, t + (t >> 4) + 272 * r),
+        ("F1->F2", 256 * (t >> 4) + 16 * r + (t & 15), t + (t >> 4) + 272 * r, c + 256 * r, cb + 17 * r),
+        ("I0->I1", 16 * c + r, cb + 17 * r, t + 256 * r, ib + 272 * r),
+        ("I1->I2", 256 * (t >> 4) + 16 * r + (t & 15), ib + 272 * r, t + 256 * r, 17 * t + r),
+    ]
+
+
+def test_inplace_layout_delivers_every_element():
+    for name, se, ss, le, ls in _layout(P.read_header()):
+        slot = {}
+        for e, s in zip(se.ravel(), ss.ravel()):
+            assert e not in slot and s not in slot.values(), name
+            slot[int(e)] = int(s)
+        assert sorted(slot) == list(range(4096)), name
+        assert max(slot.values()) < 4352, name                 # kFsLds
+        for e, s in zip(le.ravel(), ls.ravel()):
+            assert slot[int(e)] == int(s), f"{name}: element {e}"
+
+
+def test_inplace_layout_writes_where_it_read():
+    lay = _layout(P.read_header())
+    for i in range(4):
+        _, _, _, _, reads = lay[i]
+        _, _, writes, _, _ = lay[(i + 1) % 4]             # the next exchange's stores (I2 -> next F0)
+        for t in range(256):
+            assert set(writes[t].tolist()) == set(reads[t].tolist()), (lay[i][0], t)
+
+
+def _conflicts(slots, group):
+    """extra LDS cycles of one ds_*_b64 instruction per wave: lane groups of `group` lanes, a slot
+    = 2 banks of (a/4) mod 64 (reads, 32-lane groups) or mod 32 (writes, 16-lane groups)"""
+    nb = 32 if group == 32 else 16
+    tot = 0
+    for g0 in range(0, 256, group):
+        keys = [int(s) % nb for s in slots[g0:g0 + group]]
+        tot += sum(v - 1 for v in __import__("collections").Counter(keys).values())
+    return tot
+
+
+def test_inplace_layout_bank_conflicts():
+    # per instruction (one register r), summed over the 4 waves: F0 stores, F1 stores, I1 stores,
+    # I2 loads conflict-free; F1 and I1 loads one 2-way per 32 lanes; F2 loads one per 32 lanes and
+    # I0 stores one per 16 lanes (free inside a ds_write_b64, MI355X_MICROARCH.md LDS table)
+    lay = _layout(P.read_header())
+    want = {("F0->F1", "st"): 0, ("F0->F1", "ld"): 8, ("F1->F2", "st"): 0, ("F1->F2", "ld"): 8,
+            ("I0->I1", "st"): 16, ("I0->I1", "ld"): 8, ("I1->I2", "st"): 0, ("I1->I2", "ld"): 0}
+    for name, _, ss, _, ls in lay:
+        for r in range(16):
+            assert _conflicts(ss[:, r], 16) == want[(name, "st")], (name, "st", r)
+            assert _conflicts(ls[:, r], 32) == want[(name, "ld")], (name, "ld", r)
 
 
 @pytest.mark.parametrize("tb", [0, 4, 284, 1024, 1228, 2048, 3888, 4092])

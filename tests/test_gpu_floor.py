@@ -93,11 +93,15 @@ def test_float32_floor(oracle, d, tb, lsb, rand):
 # near or above 1e-5 (the port: 4e-6 .. 6e-5 over the draws below).  Such a draw is held to the
 # float32 floor itself: the HIP error against the f64 oracle next to the error of the oracle's
 # float32 port of the reference algorithm (radix-4 Stockham with exactly rounded table twiddles,
-# the class of FFTW's float path, impl.hpp:88, 98) on the same input.  The ratio of the two is
-# float32 noise, draw by draw (tools/fp32_model.py: equivalent reorderings of the kernel's own
-# arithmetic move it by +-40 %), so the bar is on the distribution: over the draws the geometric
-# mean of HIP / port must not exceed 1 (HIP at least as accurate as the port on average) and no
-# single draw may exceed 2x the port.  The sweep's three leakage-only draws come first.
+# the class of FFTW's float path, impl.hpp:88, 98) on the same input, each draw within
+# FLOOR_FACTOR (1.2) x the port, as the floor cases above, and the geometric mean over the draws
+# at most 1.  The error is the forward FFT's float32 noise (tools/fp32_model.py: an exact forward
+# transform leaves < 1.3e-7); its ratio to the port's moves by +-40 % between equivalent
+# reorderings, so the HIP path has to be more accurate than the port on average to stay under
+# 1.2x on every draw: forward pass 2's twiddles from six exactly rounded anchors
+# (fft_device.hpp twiddle_anchor6, round 5) give geomean 0.82, max 1.16 over these 24 draws on
+# the GPU (profiles/r05/parity/floor_anchor6.jsonl; the three-term recurrence before it: 0.92,
+# max 1.41).  The sweep's three leakage-only draws come first.
 SWEEP_LEAK_DRAWS = [(3, 2708, 0, 4, 310165425), (5, 2408, 1, 3, 546231597), (5, 2044, 0, 3, 826057796)]
 LEAK_DB = -40.0
 
@@ -144,7 +148,7 @@ def test_leakage_draws_at_float32_floor(oracle):
             _record(row)
             print(json.dumps(row))
             ratios.append(row["ratio"])
-            assert row["ratio"] <= 2.0, row
+            assert row["ratio"] <= FLOOR_FACTOR, row
     gm = float(np.exp(np.mean(np.log(ratios))))
     _record({"test": "leakage draws: geometric mean HIP / port", "n": len(ratios), "geomean": gm,
              "max": float(np.max(ratios)), "median": float(np.median(ratios))})

@@ -1,8 +1,9 @@
 #!/bin/bash
-# Build an ablation (timing-only) copy of the working tree's library: build/ab/NAME.so, with the
-# Python-regex substitutions of PATCHFILE applied to its copy of csrc/ (each line of PATCHFILE:
-# FILE<TAB>REGEX<TAB>REPLACEMENT; each must match).  Ablations compute wrong results on purpose:
-# they attribute a kernel's time to one of its parts in tools/ab_libs.py runs, never ship.
+# Build a variant copy of the working tree's library: build/ab/NAME.so, with PATCHFILE applied to
+# its copy of csrc/: a .txt of Python-regex substitutions (each line FILE<TAB>REGEX<TAB>REPLACEMENT,
+# each must match), or a .py script run with the copy's csrc path as argv[1].  Ablations compute
+# wrong results on purpose (they attribute a kernel's time to one of its parts in tools/ab_libs.py
+# runs); candidate variants must match the product's output within tolerance.  Neither ships.
 #   tools/build_ablation.sh NAME PATCHFILE
 set -e
 R=$(cd "$(dirname "$0")/.." && pwd)
@@ -10,6 +11,7 @@ NAME=$1; PATCH=$2
 S=$R/build/ab/src_$NAME
 rm -rf "$S"; mkdir -p "$S"
 cp -r "$R/extio_sddc_amd/csrc" "$R/include" "$S/"
+if [ "${PATCH%.py}" != "$PATCH" ]; then python3 "$PATCH" "$S/csrc"; else
 python3 - "$S/csrc" "$PATCH" <<'PY'
 import re, sys
 root, patch = sys.argv[1], sys.argv[2]
@@ -24,4 +26,5 @@ for line in open(patch):
     assert n > 0, f"{f}: no match for {rx}"
     open(p, "w").write(s2)
 PY
+fi
 bash "$R/tools/build_src_lib.sh" "$NAME"
