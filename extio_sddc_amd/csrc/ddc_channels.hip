@@ -228,6 +228,11 @@ __global__ __launch_bounds__(NT, 2) void r2iq_channels_v2_kernel(
         const int cbeg = chunk * CHUNK;
         const int cend = min(cbeg + CHUNK, nch);
         float2 *wg = work + g * N;
+        // per-slice XOR key of the pass A stores and pass B loads: channels that share a 16-lane
+        // store group or a 32-lane load group (TPC lanes each) land on disjoint banks.  Without
+        // it every pass-B load at d = 4 was a 2-way conflict (the two channels of a 32-lane group
+        // on the same 16 slots), as were d = 5, 6 stores and loads (tools/channel_banks.py)
+        const unsigned kg = 8u * (unsigned)(TPC * (g & (16 / TPC - 1)) + 16 * ((g / (16 / TPC)) & 1));
         for (int cg = cbeg; cg < cend; cg += G) {
             const int c = cg + g;
             const bool cok = c < cend;
@@ -252,7 +257,7 @@ __global__ __launch_bounds__(NT, 2) void r2iq_channels_v2_kernel(
                 float2 u[16];
                 dft16<+1>(a, u);
 #pragma unroll
-                for (int r = 0; r < 16; r++) LX(wg, 16 * l, r) = u[r];
+                for (int r = 0; r < 16; r++) lds_x(wg, (8u * (unsigned)swz(16 * l)) ^ kg, r) = u[r];
             }
             channel_sync();
             // pass B: radix-RB Stockham step (NS = 16), twiddles W_N^{j q} = W_256^{(256/N) j q}
@@ -267,7 +272,7 @@ __global__ __launch_bounds__(NT, 2) void r2iq_channels_v2_kernel(
                     const int j = l + TPC * b;
                     float2 a[RB];
 #pragma unroll
-                    for (int q = 0; q < RB; q++) a[q] = LX(wg, j, 16 * q);
+                    for (int q = 0; q < RB; q++) a[q] = lds_x(wg, (8u * (unsigned)swz(j)) ^ kg, 16 * q);
 #pragma unroll
                     for (int q = 1; q < RB; q++) a[q] = cmulc(a[q], twl[((256 / N) * q - 1) * 16 + j]);
                     dft<RB, +1>(a, y[b]);
@@ -339,7 +344,7 @@ __global__ __launch_bounds__(NT, 2) void r2iq_channels_v2_kernel(
                     const int j = l + TPC * b;          // butterfly 0..15
                     float2 a[RB], y[RB];
 #pragma unroll
-                    for (int q = 0; q < RB; q++) a[q] = LX(wg, j, 16 * q);
+                    for (int q = 0; q < RB; q++) a[q] = lds_x(wg, (8u * (unsigned)swz(j)) ^ kg, 16 * q);
 #pragma unroll
                     for (int q = 1; q < RB; q++) a[q] = cmulc(a[q], twl[((256 / N) * q - 1) * 16 + j]);
                     dft<RB, +1>(a, y);
