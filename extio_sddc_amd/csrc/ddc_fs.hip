@@ -222,10 +222,10 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
                 }
             dft16<-1>(a, v);
         }
-        // no barrier: this thread's row 17 t .. 17 t + 15 is exactly what it read in the previous
-        // frame's inverse pass 2 (every exchange writes in place of its own reads)
+        // no barrier: this thread's row is exactly what it read in the previous frame's inverse
+        // pass 2 (every exchange writes in place of its own reads)
         {
-            float2 *const row = lds + 17 * t;
+            float2 *const row = lds + 17 * t + (t >= 128);
 #pragma unroll
             for (int r = 0; r < 16; r++) row[r] = v[r];
         }
@@ -235,16 +235,16 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
             float2 a[16];
             const float2 *const col = lds + t + (t >> 4);
 #pragma unroll
-            for (int r = 0; r < 16; r++) XRD(a[r], col[272 * r]);
+            for (int r = 0; r < 16; r++) XRD(a[r], col[272 * r + (r >= 8)]);
             table_twiddle<-1, true>(a, twl, 16, x15);
             dft16<-1>(a, v);
         }
         {
             // in place of the reads (no barrier): element 256 (t >> 4) + 16 r + x15 at
-            // t + (t >> 4) + 272 r, ds_write_b64 groups of 16 lanes conflict-free
+            // t + (t >> 4) + 272 r + [r >= 8], ds_write_b64 groups of 16 lanes conflict-free
             float2 *const col = lds + t + (t >> 4);
 #pragma unroll
-            for (int r = 0; r < 16; r++) col[272 * r] = v[r];
+            for (int r = 0; r < 16; r++) col[272 * r + (r >= 8)] = v[r];
         }
         ST_SYNC(3);
         if constexpr (SCHED == kSchedSteal)
@@ -263,8 +263,9 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
         {
             float2 a[16];
             // element c + 256 g (F1 thread 16 g + (c & 15), its output c >> 4) at
-            // 272 (c >> 4) + (c & 15) + 17 g: base + immediate; banks c mod 32 (kFsPerm)
-            const float2 *const cb = lds + 272 * (c >> 4) + (c & 15);
+            // 272 (c >> 4) + (c & 15) + [c >= 128] + 17 g: base + immediate; banks
+            // (c + [c >= 128]) mod 32, conflict-free with kFsPerm (tools/fs_perm.py)
+            const float2 *const cb = lds + 272 * (c >> 4) + (c & 15) + (c >= 128);
 #pragma unroll
             for (int r = 0; r < 16; r++) XRD(a[r], cb[17 * r]);
             const float2 fw1 = wtab[c], fw4 = wtab[NT + c];   // W^c, W^{4c}
@@ -326,11 +327,10 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
         }
         {
             // in place of this thread's F2 reads (no barrier): output r at 272 (c >> 4) + (c & 15)
-            // + 17 r; banks c mod 16 per 16 lanes, the pairs c, -c with c = 0 mod 8 sharing one
-            // (a 2-way conflict inside a ds_write_b64 group costs no time: its transfer is longer)
+            // + [c >= 128] + 17 r; banks (c + [c >= 128]) mod 16 per 16 lanes, conflict-free
             int c1 = c;
             asm volatile("" : "+v"(c1));
-            float2 *const cb = lds + 272 * (c1 >> 4) + (c1 & 15);
+            float2 *const cb = lds + 272 * (c1 >> 4) + (c1 & 15) + (c1 >= 128);
 #pragma unroll
             for (int r = 0; r < 16; r++) cb[17 * r] = u[r];
         }
@@ -350,10 +350,11 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
         {
             float2 a[16];
             // element t + 256 r was stored by I0 column (t >> 4) + 16 r (its output t & 15) at
-            // 272 r + (t >> 4) + 17 (t & 15): base + immediate, one 2-way bank conflict per 32 lanes
+            // 272 r + [r >= 8] + (t >> 4) + 17 (t & 15): base + immediate, one 2-way bank conflict
+            // per 32 lanes (as F1's loads)
             const float2 *const ib = lds + (t >> 4) + 17 * x15;
 #pragma unroll
-            for (int r = 0; r < 16; r++) XRD(a[r], ib[272 * r]);
+            for (int r = 0; r < 16; r++) XRD(a[r], ib[272 * r + (r >= 8)]);
             // the next frame's number is read behind the data reads (its LDS round trip under
             // theirs), and its input loads are issued here rather than in F0, so their 16
             // registers are free through F2 and the split
@@ -377,7 +378,7 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
             asm volatile("" : "+v"(t1));
             float2 *const ib = lds + (t1 >> 4) + 17 * (t1 & 15);
 #pragma unroll
-            for (int r = 0; r < 16; r++) ib[272 * r] = u[r];
+            for (int r = 0; r < 16; r++) ib[272 * r + (r >= 8)] = u[r];
         }
         ST_SYNC(7);
         // ---- I2 (R16, NS256): twiddles g_t W^{-t r}, quarter turns, overlap-discard ----
@@ -385,7 +386,7 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
             float2 a[16];
             // element t + 256 r (I1 thread 16 r + (t & 15), its output t >> 4) at 17 t + r: the
             // next frame's F0 row of this thread, conflict-free
-            const float2 *const rb = lds + 17 * t;
+            const float2 *const rb = lds + 17 * t + (t >= 128);
 #pragma unroll
             for (int r = 0; r < 16; r++) XRD(a[r], rb[r]);
             const float2 rw1 = wtab[t], rw4 = wtab[NT + t];   // W^t, W^{4t}

@@ -21,8 +21,8 @@ def test_perm_header_is_a_lane_paired_permutation():
     cols = P.read_header()
     assert P.valid(cols)
     wr, rd = P.conflicts(cols)
-    # the in-place layout's floor: one conflict per lane group, from the pairs c = -c
-    assert (wr, rd) == P.BEST["inplace"]
+    # the in-place layout's F2 loads and I0 stores: conflict-free (keys (c + [c >= 128]) mod 32, 16)
+    assert (wr, rd) == P.BEST["inplace"] == (0, 0)
 
 
 # The in-place LDS layout of the FS kernel (round 5): every exchange's writer stores into exactly
@@ -32,14 +32,16 @@ def _layout(perm):
     t = np.arange(256)[:, None]
     r = np.arange(16)[None, :]
     c = np.asarray(perm)[:, None]
-    cb = 272 * (c >> 4) + (c & 15)
+    hi = (r >= 8).astype(int)                     # the padding map's + [e >= 2048]
+    cb = 272 * (c >> 4) + (c & 15) + (c >= 128)
     ib = (t >> 4) + 17 * (t & 15)
+    fb = 17 * t + (t >= 128)
     return [
         # (name, store element, store slot, load element, load slot)
-        ("F0->F1", 16 * t + r, 17 * t + r, t + 256 * r, t + (t >> 4) + 272 * r),
-        ("F1->F2", 256 * (t >> 4) + 16 * r + (t & 15), t + (t >> 4) + 272 * r, c + 256 * r, cb + 17 * r),
-        ("I0->I1", 16 * c + r, cb + 17 * r, t + 256 * r, ib + 272 * r),
-        ("I1->I2", 256 * (t >> 4) + 16 * r + (t & 15), ib + 272 * r, t + 256 * r, 17 * t + r),
+        ("F0->F1", 16 * t + r, fb + r, t + 256 * r, t + (t >> 4) + 272 * r + hi),
+        ("F1->F2", 256 * (t >> 4) + 16 * r + (t & 15), t + (t >> 4) + 272 * r + hi, c + 256 * r, cb + 17 * r),
+        ("I0->I1", 16 * c + r, cb + 17 * r, t + 256 * r, ib + 272 * r + hi),
+        ("I1->I2", 256 * (t >> 4) + 16 * r + (t & 15), ib + 272 * r + hi, t + 256 * r, fb + r),
     ]
 
 
@@ -76,12 +78,12 @@ def _conflicts(slots, group):
 
 
 def test_inplace_layout_bank_conflicts():
-    # per instruction (one register r), summed over the 4 waves: F0 stores, F1 stores, I1 stores,
-    # I2 loads conflict-free; F1 and I1 loads one 2-way per 32 lanes; F2 loads one per 32 lanes and
-    # I0 stores one per 16 lanes (free inside a ds_write_b64, MI355X_MICROARCH.md LDS table)
+    # per instruction (one register r), summed over the 4 waves: every store and the F2 / I2 loads
+    # conflict-free; the F1 and I1 loads one 2-way per 32 lanes (the 17-slot rows: t + (t >> 4)
+    # wraps once per 32 lanes), as the round-4 layout's F1 loads
     lay = _layout(P.read_header())
-    want = {("F0->F1", "st"): 0, ("F0->F1", "ld"): 8, ("F1->F2", "st"): 0, ("F1->F2", "ld"): 8,
-            ("I0->I1", "st"): 16, ("I0->I1", "ld"): 8, ("I1->I2", "st"): 0, ("I1->I2", "ld"): 0}
+    want = {("F0->F1", "st"): 0, ("F0->F1", "ld"): 8, ("F1->F2", "st"): 0, ("F1->F2", "ld"): 0,
+            ("I0->I1", "st"): 0, ("I0->I1", "ld"): 8, ("I1->I2", "st"): 0, ("I1->I2", "ld"): 0}
     for name, _, ss, _, ls in lay:
         for r in range(16):
             assert _conflicts(ss[:, r], 16) == want[(name, "st")], (name, "st", r)
