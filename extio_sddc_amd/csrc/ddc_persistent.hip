@@ -221,7 +221,10 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
     // 38.7 KB, still 4 workgroups per CU.
     constexpr bool WINV = N <= 1024;
     constexpr bool SEPB = N <= 256;
-    __shared__ __attribute__((aligned(16))) float2 sb[SEPB ? N : 1];
+    // N <= 256 (d >= 4): the bins of TB frames, whose tails run side by side on TB waves (below):
+    // TB = 2 at d = 4 (LDS 40.8 KB), 4 at d = 5, 6 (39.7 / 37.2 KB), still 4 workgroups per CU
+    constexpr int TB = N == 256 ? 2 : 4;
+    __shared__ __attribute__((aligned(16))) float2 sb[SEPB ? TB * N : 1];
 
     const int tid = (int)threadIdx.x;
     const int G = (int)gridDim.x, w = (int)blockIdx.x;
@@ -276,6 +279,8 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
 
     __syncthreads();   // s_first, s_next
     int f = s_first;
+    int fi = 0;                 // frames done by this workgroup (N <= 256: the slot in the batch of TB)
+    int pfb0 = 0, pfb1 = 0, pfb2 = 0, pkc0 = 0, pkc1 = 0, pkc2 = 0;   // the batch's earlier frames (output base, k)
     int blk = f / FRAMES, k = f - blk * FRAMES;
     int x[16];
     if (f >= 0) load_frame(in32, blk, k, x);
@@ -523,18 +528,35 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
                 const int bin = tunebin + m - (m >= N / 2 ? N : 0);
                 tv = split_pq(w0[bin & (HALF - 1)], w0[(HALF - bin) & (HALF - 1)], pqz[m]);
             }
-            // the N filtered bins to sb, then wave 0 runs the inverse as Stockham passes
-            if (t < N) sb[tail_swz<N>(t)] = tv;
+            // The N filtered bins to sb, and the inverse as Stockham passes on one wave (the tail).
+            // Frames go in batches of TB: frame j of a batch leaves its bins in sb[jN .. (j+1)N)
+            // and its tail for later; after the batch's last frame, wave j runs frame j's tail,
+            // the TB tails side by side.  One frame's tail ran on wave 0 while waves 1..3 waited
+            // at the next frame's first barrier (≈20 % of their frame at d = 4,
+            // profiles/r05/stamps/stamps_p_d4.txt); batched, that wait comes once per TB frames.
+            // A range's last frames (fewer than TB) run theirs at its last frame.
+            const int slot = fi & (TB - 1);
+            if (t < N) sb[N * slot + tail_swz<N>(t)] = tv;
             ST_SYNC(6);
-            if (t < 64) {
+            const int fbase = oblk + emit_base<N>(kc);
+            const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+            if ((slot == TB - 1 || fn < 0) && wv <= slot) {
                 float2 u[8];
                 const float2 *twq = twl + 15 * 16;
-                tail_pass<N, 0>(sb, twq, t, u);
-                tail_pass<N, 1>(sb, twq, t, u);
-                tail_pass<N, 2>(sb, twq, t, u);
-                if constexpr (tail_passes<N>() == 4) tail_pass<N, 3>(sb, twq, t, u);
-                tail_emit<N, NCO, CS16>(out, oblk + emit_base<N>(kc), kc, t, u, oa, nco);
+                float2 *const sbw = sb + N * wv;
+                const int lt = t & 63;
+                tail_pass<N, 0>(sbw, twq, lt, u);
+                tail_pass<N, 1>(sbw, twq, lt, u);
+                tail_pass<N, 2>(sbw, twq, lt, u);
+                if constexpr (tail_passes<N>() == 4) tail_pass<N, 3>(sbw, twq, lt, u);
+                const int ob = wv == slot ? fbase : wv == 0 ? pfb0 : wv == 1 ? pfb1 : pfb2;
+                const int ok = wv == slot ? kc : wv == 0 ? pkc0 : wv == 1 ? pkc1 : pkc2;
+                tail_emit<N, NCO, CS16>(out, ob, ok, lt, u, oa, nco);
             }
+            if (slot == 0) pfb0 = fbase, pkc0 = kc;
+            else if (slot == 1) pfb1 = fbase, pkc1 = kc;
+            else if (slot == 2) pfb2 = fbase, pkc2 = kc;
+            fi++;
         }
         ST_FRAME_END();
         f = fn;
