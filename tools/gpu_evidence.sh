@@ -1,8 +1,10 @@
 #!/bin/bash
 # Round evidence on one box, each GPU step under its own time limit, stopping at the first
 # crash-like exit: GPU tests, smoke, the driver's exact bench command, a rocprofv3
-# kernel-trace --stats run of that same command, and PMC passes (kernel-trace only, one
-# counter group per run) for the headline kernel: VALU issue and HBM bytes.  Arg: TAG.
+# kernel-trace --stats run of that same command, then tools/gpu_pmc_configs.sh (PMC passes,
+# kernel-trace only, one counter group per run, for every config the bench reports).  Arg: TAG.
+#   gpurun --timeout 1200 -- 'bash tools/gpu_evidence.sh r05_final'
+#   bash tools/save_evidence.sh r05_final r05/final
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"; TAG=${1:-round}; O=$R/gpurun_out/$TAG; mkdir -p $O
@@ -14,18 +16,9 @@ if [ -z "$SKIP_TESTS" ]; then
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit $?
 fi
 timeout -k 10 300 python $BENCH > $O/bench.log 2>&1 || exit $?
+echo "bench done"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python3 $R/$BENCH > $O/trace.log 2>&1 || exit $?
-P="python3 $R/bench.py --steps 5 --warmup 2 --warmup-ms 0 --no-cpu-baseline --no-sweep"
-timeout -k 10 120 rocprofv3 --kernel-trace --output-format csv --kernel-include-regex r2iq_persistent \
-  --pmc SQ_INSTS_VALU SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE \
-  -d $O/pmc_valu -o run -- $P > $O/pmc_valu.log 2>&1 || exit $?
-for c in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 120 rocprofv3 --kernel-trace --output-format csv --kernel-include-regex r2iq_persistent --pmc $c \
-    -d $O/pmc_$c -o run -- $P > $O/pmc_$c.log 2>&1 || exit $?
-done
-for c in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 120 rocprofv3 --kernel-trace --output-format csv --kernel-include-regex calib --pmc $c \
-    -d $O/calib_$c -o run -- $R/build/bin/pmc_calib > $O/calib_$c.log 2>&1 || exit $?
-done
+echo "trace done"
+[ -n "$SKIP_PMC" ] || bash $R/tools/gpu_pmc_configs.sh $O/pmc || exit $?
 echo done > $O/DONE
