@@ -28,8 +28,8 @@
 // tools/fs_model.py models the frame step by step against the f64 oracle.
 //
 // Layout for MI355X: one 256-thread workgroup (4 wave64) per frame in flight, 4 workgroups per
-// CU (40 836 B of LDS each fill the 160 KB), persistent grid (CUs x 4) fed by the static-prefix
-// + dynamic-suffix frame schedule of ddc_queue.hpp, the next frame's input prefetched into
+// CU (40 852 B of LDS each fill the 160 KB), persistent grid (CUs x 4) fed by the slot-weighted
+// static frame split of ddc_queue.hpp (queue, work stealing: options), the next frame's input prefetched into
 // registers under inverse pass 1, all global memory through raw buffer instructions (scalar base
 // + lane offset), nt IQ stores.
 #include <hip/hip_runtime.h>
@@ -128,9 +128,14 @@ constexpr int kQWave = 3;
 // t + 256 r at t + (t >> 4) + 272 r are base + immediate too, with one 2-way bank conflict per
 // 32-lane group.  The other exchanges use the first 4096 slots with XOR keys.
 constexpr int kFsLds = HALF + HALF / 16;
+// twiddle bases W^j (j < 256) at j + [j >= 128], W^{4j} kFsTw later: F2 reads them at its column
+// c = kFsPerm[t], whose key c + [c >= 128] the permutation keeps distinct mod 32 over 32 lanes
+// (tools/fs_perm.py), I2 at t; both ds_read_b64 and conflict-free.  (Unpadded, the lane pairs
+// c, 256 - c with c = 0 mod 16 hit one bank.)
+constexpr int kFsTw = NT + 1;
 
-// the frame schedules (ddc_queue.hpp): the slot-weighted static split alone, the static prefix +
-// dynamic queue (round 3/4), work stealing over the static split (default since round 5)
+// the frame schedules (ddc_queue.hpp): the slot-weighted static split alone (the default), the
+// static prefix + dynamic queue (round 3/4), work stealing over the static split (round 5)
 enum { kSchedStatic = 0, kSchedQueue = 1, kSchedSteal = 2 };
 template <int SCHED> struct SchedOf { using T = StealSchedule; };
 template <> struct SchedOf<kSchedStatic> { using T = StaticSchedule; };
@@ -155,9 +160,9 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
     // its thread index).  In LDS, not registers or L2: the L2 loads' waits (vmcnt, in issue
     // order) would also wait for the input prefetch and the stores.
     __shared__ __attribute__((aligned(16))) float2 twl[15 * 16];
-    __shared__ __attribute__((aligned(16))) float2 wtab[2 * NT];
+    __shared__ __attribute__((aligned(16))) float2 wtab[2 * kFsTw];
     __shared__ int s_next;   // the workgroup's next frame (the queue wave's schedule), -1 when none is left
-    static_assert(sizeof(float2) * (kFsLds + 15 * 16 + 2 * NT) + sizeof(int) <= 163840 / 4,
+    static_assert(sizeof(float2) * (kFsLds + 15 * 16 + 2 * kFsTw) + sizeof(int) <= 163840 / 4,
                   "four workgroups per CU");
 
     const int tid = (int)threadIdx.x;
@@ -181,8 +186,8 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
             if (tid == QLANE) s_next = f0[0];
         }
         for (int i = tid; i < 15 * 16; i += NT) twl[i] = tw_p1[i];
-        wtab[tid] = rec_f[tid];
-        wtab[NT + tid] = rec_f[NT + tid];
+        wtab[tid + (tid >= 128)] = rec_f[tid];
+        wtab[kFsTw + tid + (tid >= 128)] = rec_f[NT + tid];
         __syncthreads();
         const int f = s_next;
         if (f >= 0 && f0s < 0) load_frame(in32, f / FRAMES, f % FRAMES, x);
@@ -268,7 +273,8 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
             const float2 *const cb = lds + 272 * (c >> 4) + (c & 15) + (c >= 128);
 #pragma unroll
             for (int r = 0; r < 16; r++) XRD(a[r], cb[17 * r]);
-            const float2 fw1 = wtab[c], fw4 = wtab[NT + c];   // W^c, W^{4c}
+            const int cw = c + (c >= 128);
+            const float2 fw1 = wtab[cw], fw4 = wtab[kFsTw + cw];   // W^c, W^{4c}
             twiddle_rec16<-1>(a, fw1, fw4);
             dft16<-1>(a, v);
         }
@@ -389,7 +395,8 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
             const float2 *const rb = lds + 17 * t + (t >= 128);
 #pragma unroll
             for (int r = 0; r < 16; r++) XRD(a[r], rb[r]);
-            const float2 rw1 = wtab[t], rw4 = wtab[NT + t];   // W^t, W^{4t}
+            const int tw = t + (t >= 128);
+            const float2 rw1 = wtab[tw], rw4 = wtab[kFsTw + tw];   // W^t, W^{4t}
             twiddle_g16<+1>(a, g0, g1, g4, rw1, rw4);
             dft16<+1>(a, u);
             const int fb = oblk + emit_base<HALF>(kc);

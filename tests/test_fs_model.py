@@ -20,9 +20,12 @@ from extio_sddc_amd.synth import make_stream  # noqa: E402
 def test_perm_header_is_a_lane_paired_permutation():
     cols = P.read_header()
     assert P.valid(cols)
-    wr, rd = P.conflicts(cols)
-    # the in-place layout's F2 loads and I0 stores: conflict-free (keys (c + [c >= 128]) mod 32, 16)
-    assert (wr, rd) == P.BEST["inplace"] == (0, 0)
+    # the in-place layout's I0 stores, F2 loads and F2 twiddle-base loads (W^c at c + [c >= 128]):
+    # conflict-free (keys (c + [c >= 128]) mod 16, 32, 32)
+    assert P.conflicts(cols) == P.BEST["inplace"] == (0, 0, 0)
+    # the unpadded twiddle table (key c mod 32) would not be: pairs c, 256 - c = 0 mod 16 collide
+    c = np.asarray(cols)
+    assert _conflicts(c, 32) > 0 and _conflicts(c + (c >= 128), 32) == 0
 
 
 # The in-place LDS layout of the FS kernel (round 5): every exchange's writer stores into exactly

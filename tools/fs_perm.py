@@ -1,60 +1,55 @@
 #!/usr/bin/env python3
-"""Lane -> column permutation of the d = 0 fused-split kernel (ddc_persistent.hip, FS).
+"""Lane -> column permutation of the d = 0 fused-split kernel (ddc_fs.hip, r2iq_fs_kernel).
 
 Lanes 2p, 2p + 1 hold forward-pass-2 columns c, 256 - c (lanes 0, 1: the self-mirrored 0, 128),
 so the split's mirror bins are one DPP quad_perm [1,0,3,2] away.  Which pair goes to which lane
-pair sets the LDS bank pattern of two exchanges:
-  * forward pass 2 reads element c + 256 r at swz(c) + 256 r (ds_read_b64, lane groups of 32):
-    conflict-free iff swz(c) mod 32 is distinct over each 32 lanes;
-  * inverse pass 0 stores element 16 c + k at 16 c + (k ^ (swz(c) & 15)) (ds_write_b64, groups of
-    16): conflict-free iff swz(c) mod 16 is distinct over each 16 lanes.  (With the plain key
-    c & 15 the pairs with c = 0 or 8 mod 16 have c = -c mod 16, forcing one 2-way conflict per 16
-    lanes; the XOR with c >> 4 in swz lifts that at one v_xor per inverse pass-1 read.)
-Simulated annealing over the assignment; writes extio_sddc_amd/csrc/ddc_fs_perm.h.
+pair sets the LDS bank pattern of three accesses (MI355X_MICROARCH.md, LDS: a ds_read_b64 serves
+lane groups of 32 over 64 banks, so slot s = 8-byte index is conflict-free iff s mod 32 is distinct
+over the group; ds_write_b64 / ds_write2_b64 serve groups of 16 over 32 banks: s mod 16 distinct):
+  * forward pass 2 reads its column's 16 elements, one ds_read_b64 per register (groups of 32);
+  * inverse pass 0 stores its 16 outputs in place of those reads (groups of 16);
+  * forward pass 2 reads its twiddle bases W^c, W^{4c} (ds_read_b64, groups of 32).
+The assignment is solved exactly as a 0/1 program (scipy's HiGHS MILP): pair p goes to one
+16-lane half of one 32-lane group, each half takes 8 pairs, and the objective is the extra LDS
+cycles per frame (16 reads and 16 stores per frame at the exchange, 2 twiddle-base reads).
+Writes extio_sddc_amd/csrc/ddc_fs_perm.h.
 
-  python tools/fs_perm.py [--seed S] [--iters N] [--check]
+  python tools/fs_perm.py [--check]
 """
 from __future__ import annotations
 
 import argparse
-import math
 import os
-import random
 from collections import Counter
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HDR = os.path.join(ROOT, "extio_sddc_amd", "csrc", "ddc_fs_perm.h")
 
-
-def swz(e: int) -> int:
-    return e ^ ((e >> 4) & 15)
-
-
 LAYOUT = "inplace"   # the product's layout (round 5)
-BEST = {"xor": (0, 0), "pad": (0, 0), "inplace": (0, 0)}   # the fewest conflicts a layout allows
+# the fewest extra cycles (I0 stores, F2 reads, twiddle-base reads) per instruction and workgroup
+BEST = {"inplace": (0, 0, 0)}
+WEIGHTS = (16, 16, 2)   # instructions per frame of each access
 
 
 def keys(c: int):
-    """(inverse pass-0 store bank key mod 16, forward pass-2 read bank key mod 32) of column c"""
-    if LAYOUT == "inplace":
-        # in-place exchanges (round 5): F2 reads element c + 256 g at P(16 g + (c & 15) + 256 (c >> 4))
-        # = 272 (c >> 4) + (c & 15) + [c >= 128] + 17 g with the padding map P(e) = e + (e >> 4)
-        # + [e >= 2048], and I0 stores its output r at the same slot + 17 r: keys (c + [c >= 128])
-        # mod 16 and mod 32.  The odd extra pad of the upper half keeps the lane pairs c, 256 - c
-        # apart (c = 1 - c mod 2^k has no solution), so both can be conflict-free.
-        k = c + (c >= 128)
-        return k % 16, k % 32
-    if LAYOUT == "pad":
-        # padded exchanges: F2 reads element c + 256 r at e + (e >> 4); I0 row c at 16 c + c + [c >= 128]
-        return (c + (c >= 128)) % 16, (c + (c >> 4)) % 32
-    return swz(c) & 15, swz(c) % 32
+    """(inverse pass-0 store key mod 16, forward pass-2 read key mod 32, twiddle-base read key
+    mod 32) of column c"""
+    # in-place exchanges (round 5): F2 reads element c + 256 g at 272 (c >> 4) + (c & 15)
+    # + [c >= 128] + 17 g, and I0 stores its output r at the same slot + 17 r: keys c + [c >= 128].
+    # The odd extra pad of the upper half keeps the lane pairs c, 256 - c apart (c = 1 - c mod 2^k
+    # has no solution), so both can be conflict-free.  The twiddle bases W^j sit at j + [j >= 128]
+    # (ddc_fs.hip kFsTw), the same key, which the unpadded table (c mod 32: the pairs c = 0 mod 16
+    # share it) could not give.
+    k = c + (c >= 128)
+    return k % 16, k % 32, k % 32
 
 
 def conflicts(cols):
-    """(extra write cycles-groups, extra read cycles-groups) of a 256-lane column list"""
-    wr = sum(sum(v - 1 for v in Counter(keys(c)[0] for c in cols[16 * g:16 * g + 16]).values()) for g in range(16))
-    rd = sum(sum(v - 1 for v in Counter(keys(c)[1] for c in cols[32 * g:32 * g + 32]).values()) for g in range(8))
-    return wr, rd
+    """extra cycles per instruction over the workgroup: (I0 stores, F2 reads, twiddle-base reads)"""
+    def extra(key, n):
+        return sum(sum(v - 1 for v in Counter(keys(c)[key] for c in cols[g:g + n]).values())
+                   for g in range(0, 256, n))
+    return extra(0, 16), extra(1, 32), extra(2, 32)
 
 
 def valid(cols) -> bool:
@@ -62,38 +57,77 @@ def valid(cols) -> bool:
             and all((cols[2 * p] + cols[2 * p + 1]) % 256 == 0 for p in range(1, 128)))
 
 
-def anneal(seed: int, iters: int):
-    rng = random.Random(seed)
-    assign = [(0, 128)] + [(c, 256 - c) for c in range(1, 128)]
+def solve(time_limit: float = 600.0):
+    """minimum-weight assignment of the 128 lane pairs to (32-lane group, 16-lane half)"""
+    import numpy as np
+    from scipy.optimize import Bounds, LinearConstraint, milp
+    from scipy.sparse import lil_matrix
 
-    def flat(a):
-        return [x for p in a for x in p]
-    cur = conflicts(flat(assign))
-    cs = cur[0] + 4 * cur[1]
-    T = 3.0
-    for _ in range(iters):
-        i, j = rng.randrange(1, 128), rng.randrange(1, 128)
-        new = assign[:]
-        if rng.random() < 0.3:
-            new[i] = new[i][::-1]
-        else:
-            new[i], new[j] = new[j], new[i]
-        c = conflicts(flat(new))
-        s = c[0] + 4 * c[1]
-        if s <= cs or rng.random() < math.exp((cs - s) / T):
-            assign, cur, cs = new, c, s
-            if cur == BEST[LAYOUT]:
-                break
-        T = max(0.05, T * 0.99999)
-    return flat(assign), cur
+    pairs = [(0, 128)] + [(c, 256 - c) for c in range(1, 128)]
+    NP, NG, NH = 128, 8, 2
+    nx = NP * NG * NH
+    # slack (extra lanes on one bank) per (group, bank) for the reads, per (half, bank) for the stores
+    # (16 banks of 8 bytes for the stores: keys()[0] < 16)
+    off_rd, off_tw, off_wr = nx, nx + NG * 32, nx + 2 * NG * 32
+    n = off_wr + NG * NH * 32
+
+    def x(p, g, h):
+        return (p * NG + g) * NH + h
+
+    rows, lo, hi = [], [], []
+
+    def add(coefs, lb, ub):
+        rows.append(coefs)
+        lo.append(lb)
+        hi.append(ub)
+
+    for p in range(NP):
+        add([(x(p, g, h), 1) for g in range(NG) for h in range(NH)], 1, 1)
+    for g in range(NG):
+        for h in range(NH):
+            add([(x(p, g, h), 1) for p in range(NP)], 8, 8)
+    add([(x(0, 0, 0), 1)], 1, 1)                      # columns 0, 128 on lanes 0, 1
+
+    def hits(p, key, b):
+        return sum(1 for c in pairs[p] if keys(c)[key] == b)
+    for g in range(NG):
+        for b in range(32):
+            for key, off in ((1, off_rd), (2, off_tw)):
+                add([(x(p, g, h), hits(p, key, b)) for p in range(NP) for h in range(NH) if hits(p, key, b)]
+                    + [(off + 32 * g + b, -1)], -np.inf, 1)
+            for h in range(NH):
+                add([(x(p, g, h), hits(p, 0, b)) for p in range(NP) if hits(p, 0, b)]
+                    + [(off_wr + 32 * (NH * g + h) + b, -1)], -np.inf, 1)
+    A = lil_matrix((len(rows), n))
+    for i, r in enumerate(rows):
+        for j, v in r:
+            A[i, j] += v
+    cost = np.zeros(n)
+    cost[off_rd:off_tw] = WEIGHTS[1]
+    cost[off_tw:off_wr] = WEIGHTS[2]
+    cost[off_wr:] = WEIGHTS[0]
+    ub = np.ones(n)
+    ub[nx:] = 16
+    res = milp(cost, constraints=LinearConstraint(A.tocsr(), lo, hi), integrality=np.ones(n),
+               bounds=Bounds(0, ub), options={"time_limit": time_limit})
+    assert res.x is not None, res.message
+    sel = res.x.round().astype(int)
+    cols = []
+    for g in range(NG):
+        for h in range(NH):
+            ps = [p for p in range(NP) if sel[x(p, g, h)]]
+            for p in sorted(ps, key=lambda p: p != 0):
+                cols += list(pairs[p])
+    return cols, conflicts(cols), res.message
 
 
 def write_header(cols, cur, path=HDR):
     rows = ",\n".join("    " + ", ".join(f"{c:3d}" for c in cols[i:i + 16]) for i in range(0, 256, 16))
     with open(path, "w") as f:
         f.write(f"""// ddc_fs_perm.h — generated by tools/fs_perm.py: lane -> forward-pass-2 column of the d = 0
-// fused-split kernel (lanes 2p, 2p+1: columns c, 256 - c), for the {LAYOUT} exchange layout.  LDS bank
-// conflicts: {cur[0]} on the inverse pass-0 stores, {cur[1]} on the forward pass-2 reads.
+// fused-split kernel (lanes 2p, 2p+1: columns c, 256 - c), for the {LAYOUT} exchange layout.  Extra LDS
+// cycles per instruction and workgroup: {cur[0]} on the inverse pass-0 stores, {cur[1]} on the forward
+// pass-2 reads, {cur[2]} on the forward pass-2 twiddle-base reads (the optimum for this layout).
 #pragma once
 __constant__ int kFsPerm[256] = {{
 {rows}}};
@@ -108,23 +142,20 @@ def read_header():
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--seed", type=int, default=7)
-    ap.add_argument("--iters", type=int, default=2_000_000)
     ap.add_argument("--check", action="store_true", help="validate the committed header only")
-    ap.add_argument("--layout", choices=["xor", "pad", "inplace"], default="inplace")
+    ap.add_argument("--time-limit", type=float, default=600.0)
     ap.add_argument("--out", default=HDR)
     args = ap.parse_args()
-    global LAYOUT
-    LAYOUT = args.layout
     if args.check:
         cols = read_header()
         assert valid(cols), "not a paired permutation"
-        print("conflicts (write, read):", conflicts(cols))
+        print("extra cycles (stores, reads, twiddle reads):", conflicts(cols))
         return
-    cols, cur = anneal(args.seed, args.iters)
+    cols, cur, msg = solve(args.time_limit)
     assert valid(cols)
     write_header(cols, cur, args.out)
-    print("conflicts (write, read):", cur)
+    print(msg)
+    print("extra cycles (stores, reads, twiddle reads):", cur)
 
 
 if __name__ == "__main__":
