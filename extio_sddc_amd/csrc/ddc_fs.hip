@@ -5,12 +5,14 @@
 // r2c 8192 as a 4096-point packed complex FFT, split x shift x filter with the zero fill, the
 // inverse 4096-point FFT and the overlap-discard store, as six radix-16 passes on 256 threads
 // (16 points each) with four LDS exchanges:
-//   F0 convert + DFT-16 from registers      -> LDS (padded rows: no address VALU)
-//   F1 table twiddles + DFT-16               -> LDS (XOR-swizzled)
+//   F0 convert + DFT-16 from registers      -> LDS
+//   F1 table twiddles + DFT-16               -> LDS
 //   F2 recurrence twiddles + DFT-16, then the split x filter and I0's DFT-16 in registers
-//                                            -> LDS (XOR-keyed rows)
-//   I1 table twiddles + DFT-16               -> LDS (XOR-swizzled)
+//                                            -> LDS
+//   I1 table twiddles + DFT-16               -> LDS
 //   I2 twiddles g_t W^{-t r} + DFT-16, quarter turns, overlap-discard IQ stores.
+// Every exchange writes in place of its own reads (padded 17-slot rows, below), so a frame has
+// four barriers and every LDS access is one base plus a per-register immediate.
 //
 // The fused split.  F2's butterfly on lane l is column c = kFsPerm[l]: it produces Z[c + 256 k],
 // k = 0..15.  The split of bin b needs Z[-b]; for b = c + 256 k that is Z[(256 - c) + 256 (15 - k)],
@@ -123,10 +125,11 @@ __device__ __forceinline__ void emit_frame_q(void *__restrict__ out, int fbase, 
 
 // The queue wave (not wave 0, which also carries the self-mirrored columns' split)
 constexpr int kQWave = 3;
-// F0 -> F1 exchange: element 16 t + r (F0's row t) at 17 t + r, so F0's 16 stores are one base
-// plus an immediate each (no address VALU) and conflict-free; F1's reads of element
-// t + 256 r at t + (t >> 4) + 272 r are base + immediate too, with one 2-way bank conflict per
-// 32-lane group.  The other exchanges use the first 4096 slots with XOR keys.
+// The exchanges' LDS layout: element 16 R + j (row R, column j) at 17 R + j + [R >= 128].  F0's
+// row stores and I2's row reads are conflict-free, F2's reads and I0's stores too (with
+// kFsPerm, tools/fs_perm.py); F1's and I1's reads of 272-slot strides have one 2-way bank
+// conflict per 32 lanes, which no lane assignment removes on 17-slot rows (DESIGN.md §4.1,
+// round 5).  tests/test_fs_model.py checks every exchange's delivery and in-place property.
 constexpr int kFsLds = HALF + HALF / 16;
 // twiddle bases W^j (j < 256) at j + [j >= 128], W^{4j} kFsTw later: F2 reads them at its column
 // c = kFsPerm[t], whose key c + [c >= 128] the permutation keeps distinct mod 32 over 32 lanes
