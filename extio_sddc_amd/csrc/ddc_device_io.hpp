@@ -42,16 +42,18 @@ __device__ __forceinline__ int buf_load4(__amdgpu_buffer_rsrc_t r, unsigned voff
 #ifndef SDDC_LD_AUX
 #define SDDC_LD_AUX 0
 #endif
+template <int AUX = SDDC_ST_AUX>
 __device__ __forceinline__ void buf_store8(float2 v, __amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff)
 {
     u32x2 u;
     u.x = __float_as_uint(v.x);
     u.y = __float_as_uint(v.y);
-    __builtin_amdgcn_raw_buffer_store_b64(u, r, voff, soff, SDDC_ST_AUX);
+    __builtin_amdgcn_raw_buffer_store_b64(u, r, voff, soff, AUX);
 }
+template <int AUX = SDDC_ST_AUX>
 __device__ __forceinline__ void buf_store4(unsigned v, __amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff)
 {
-    __builtin_amdgcn_raw_buffer_store_b32(v, r, voff, soff, SDDC_ST_AUX);
+    __builtin_amdgcn_raw_buffer_store_b32(v, r, voff, soff, AUX);
 }
 
 // Fine-tune NCO on output sample o of the batch (fine_tune.h): phasor T[q-1] * S_b[l] for
@@ -96,15 +98,16 @@ __device__ __forceinline__ unsigned cs16_pack(float2 v, float scale)
 template <bool CS16>
 constexpr unsigned out_bytes() { return CS16 ? 4u : 8u; }
 
-// store complex v at element (voff_el + soff_el) of the buffer r
-template <bool CS16>
+// store complex v at element (voff_el + soff_el) of the buffer r; AUX: the cache policy (default
+// nt; 0 = write-back, for stores whose lines other waves complete, so that L2 merges them)
+template <bool CS16, int AUX = SDDC_ST_AUX>
 __device__ __forceinline__ void store_iq(float2 v, __amdgpu_buffer_rsrc_t r, unsigned voff_el, unsigned soff_el,
                                          const OutArgs &oa)
 {
     if constexpr (CS16)
-        buf_store4(cs16_pack(v, oa.scale), r, 4u * voff_el, 4u * soff_el);
+        buf_store4<AUX>(cs16_pack(v, oa.scale), r, 4u * voff_el, 4u * soff_el);
     else
-        buf_store8(v, r, 8u * voff_el, 8u * soff_el);
+        buf_store8<AUX>(v, r, 8u * voff_el, 8u * soff_el);
 }
 
 }  // namespace sddc

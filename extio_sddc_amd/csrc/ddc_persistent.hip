@@ -66,6 +66,29 @@ template <int N> __device__ __forceinline__ float2 tail_twiddle(const float2 *__
     return tw4096[(kk * r * (HALF / (R * ns))) & (HALF - 1)];
 }
 
+// d = 3 (N = 512): the inverse as two independent 256-point halves on waves 0 and 1.  With
+// m = m' + 256 s and n = 2 n' + p, y[2 n' + p] = IDFT_256(E_p)[n'], E_p[m'] = (X[m'] + (-1)^p
+// X[m' + 256]) e^{2 pi i m' p / 512}: one radix-2 step in the registers of the thread holding
+// X[m'], X[m' + 256] (the split's), then the d = 4 tail on each half.  Kept: y[0, 384) (k >= 1),
+// y[128, 384) (k = 0), i.e. u[r] = y[2 (t + 64 r) + p] for r < 3 (r >= 1 at k = 0).  The two waves'
+// stores interleave (8 bytes every 16), so they go write-back rather than nt: L2 merges the halves
+// into whole lines (nt: WRITE_SIZE +35 %; write-back: equal to the one-tail kernel's, at the same
+// speed; exchanging the halves through LDS to store whole runs needed a workgroup barrier and
+// was slower than both, profiles/r05/ab/persistent_d3_halves*.txt).
+template <bool NCO, bool CS16>
+__device__ __forceinline__ void tail_emit_half(void *__restrict__ out, int fbase, int k, int t, int p,
+                                               const float2 (&u)[8], const OutArgs &oa, const NcoArgs &nco)
+{
+    const __amdgpu_buffer_rsrc_t ro = buf_rsrc(static_cast<char *>(out) + (size_t)fbase * out_bytes<CS16>());
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+        if (r == 0 && k == 0) continue;
+        float2 v = flip(u[r], oa.lsbmask);
+        if constexpr (NCO) v = nco_mix(v, nco, fbase + 2 * (t + 64 * r) + p);
+        store_iq<CS16, 0>(v, ro, (unsigned)(2 * t + p), (unsigned)(128 * r), oa);
+    }
+}
+
 // the kept outputs of the last pass, u[r] = y[t + (N / R) r]: y[0, 3N/4) (k >= 1), y[N/4, 3N/4) (k = 0)
 template <int N, bool NCO, bool CS16>
 __device__ __forceinline__ void tail_emit(void *__restrict__ out, int fbase, int k, int t, const float2 (&u)[8],
@@ -207,11 +230,12 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
     // d = 3 and d >= 4: the inverse runs as Stockham passes on wave 0 (tail_pass); their twiddles
     // take the inverse table's place
     constexpr bool R4T = N <= 256 || N == 512;
+    constexpr int TN = N == 512 ? 256 : N;   // the tail's size (d = 3: two 256-point halves)
     // d = 2 only: the inverse as radix-4 passes on all 256 threads (wg_pass).  At d = 1 (N = 2048,
     // two butterflies per thread per pass) the same form measured 7-8 % slower than the two-wave
     // radix-16 tail (profiles/r03/ab/d12_wg.txt)
     constexpr bool WGT = N == 1024;
-    constexpr int TWQ = R4T ? tail_twn<N>() : WGT ? wg_twn<N>() : 15 * SQ;
+    constexpr int TWQ = R4T ? tail_twn<TN>() : WGT ? wg_twn<N>() : 15 * SQ;
     __shared__ __attribute__((aligned(16))) float2 twl[15 * 16 + TWQ];
     float2 *const w0 = lds, *const w1 = lds;   // the pass buffers (one 32 KB frame buffer)
     // d >= 2: the inverse's last passes run on one wave, so they are ordered within that wave
@@ -257,6 +281,8 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
     const float2 fw2_ = tw4096[(2 * fb_) & (HALF - 1)], fw3_ = tw4096[(3 * fb_) & (HALF - 1)];
     const float2 fw8_ = tw4096[(8 * fb_) & (HALF - 1)], fw12_ = tw4096[(12 * fb_) & (HALF - 1)];
     float2 iw1_ = ZROT ? rec_f[tid] : fw1_, iw4_ = ZROT ? rec_f[NT + tid] : fw4_;
+    // d = 3: the halves' twiddle e^{2 pi i t / 512} (applied as the conjugate of W_4096^{8t})
+    const float2 hw_ = N == 512 ? tw4096[(8 * tid) & (HALF - 1)] : make_float2(1.f, 0.f);
     if constexpr (N >= 512 && N < HALF) {
         if (tid < N / 16) {
             iw1_ = rec_i[tid];
@@ -267,7 +293,7 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
         if ((!R4T && !WGT) || i < 15 * 16) {
             twl[i] = i < 15 * 16 ? tw_p1[i] : tw_q1[i - 15 * 16];   // visible after the first frame's pass-0 barrier
         } else if constexpr (R4T) {
-            twl[i] = tail_twiddle<N>(tw4096, i - 15 * 16);
+            twl[i] = tail_twiddle<TN>(tw4096, i - 15 * 16);
         } else if constexpr (WGT) {
             const int e = i - 15 * 16;   // W_{4 Ns}^k, Ns = N/256 x 1, 4, 16, 64
             constexpr int r0 = N / 256;
@@ -441,20 +467,30 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
                     continue;
                 }
                 if constexpr (N == 512) {
-                    // d = 3: the 512 filtered bins (inverse input m = t + 256 r) go to LDS, and wave 0
-                    // runs the inverse as three radix-8 Stockham passes (tail_pass) instead of the
-                    // radix-2 pass on every thread and two radix-16 passes on 32 lanes
+                    // d = 3: the 512 filtered bins (inverse input m = t + 256 r) as two 256-point
+                    // halves (tail_emit_half): the radix-2 step here, then waves 0 and 1 each run
+                    // the d = 4 tail (four radix-4 Stockham passes) on one half.  One 512-point
+                    // tail on wave 0 (three radix-8 passes) held waves 1..3 at the next frame's
+                    // first barrier for twice as long.
+                    float2 hw = hw_;
+                    asm volatile("" : "+v"(hw));
+                    const float2 e0 = make_float2(a[0].x + a[1].x, a[0].y + a[1].y);
+                    const float2 e1 = TW<+1>(make_float2(a[0].x - a[1].x, a[0].y - a[1].y), hw);
                     ST_SYNC(6);   // every wave's Z reads are done
-#pragma unroll
-                    for (int r = 0; r < R0; r++) w1[tail_swz<N>(t + NT * r)] = a[r];
+                    w1[tail_swz<TN>(t)] = e0;
+                    w1[TN + tail_swz<TN>(t)] = e1;
                     ST_SYNC(7);
-                    if (t < 64) {
+                    const int p = __builtin_amdgcn_readfirstlane(tid >> 6);
+                    if (p < 2) {
+                        const int lt = t & 63;
+                        float2 *const hb = w1 + TN * p;
                         float2 v8[8];
                         const float2 *twq = twl + 15 * 16;
-                        tail_pass<N, 0>(w1, twq, t, v8);
-                        tail_pass<N, 1>(w1, twq, t, v8);
-                        tail_pass<N, 2>(w1, twq, t, v8);
-                        tail_emit<N, NCO, CS16>(out, oblk + emit_base<N>(kc), kc, t, v8, oa, nco);
+                        tail_pass<TN, 0>(hb, twq, lt, v8);
+                        tail_pass<TN, 1>(hb, twq, lt, v8);
+                        tail_pass<TN, 2>(hb, twq, lt, v8);
+                        tail_pass<TN, 3>(hb, twq, lt, v8);
+                        tail_emit_half<NCO, CS16>(out, oblk + emit_base<N>(kc), kc, lt, p, v8, oa, nco);
                     }
                     ST_FRAME_END();
                     f = fn;
