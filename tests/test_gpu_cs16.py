@@ -51,7 +51,7 @@ def _dev(torch, r, x, nblk, d, cs16):
     return o.reshape(-1, 2) if cs16 else o.view(np.complex64)
 
 
-@pytest.mark.parametrize("d,tb,lsb,rand", [(0, 1024, False, False), (1, 284, True, True),
+@pytest.mark.parametrize("d,tb,lsb,rand", [(0, 1024, False, False), (1, 284, True, True), (3, 1228, True, True),
                                            (4, 2048, False, True), (6, 4, True, False)])
 def test_single_cs16_bit_exact(torch_dev, d, tb, lsb, rand):
     nblk = 4

@@ -44,7 +44,7 @@ def _ddc(d, tb, lsb=False, rand=False):
     return r
 
 
-@pytest.mark.parametrize("d,tb,lsb,fc", [(0, 1024, False, 0.0123), (1, 284, True, -0.271),
+@pytest.mark.parametrize("d,tb,lsb,fc", [(0, 1024, False, 0.0123), (1, 284, True, -0.271), (3, 1228, True, 0.137),
                                           (4, 2048, False, 0.4999), (6, 1024, False, 1e-4)])
 def test_fused_nco_bit_exact_vs_oracle_mixer(torch_dev, oracle, d, tb, lsb, fc):
     nblk = 4 << min(d, 3)
