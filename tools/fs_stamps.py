@@ -32,10 +32,10 @@ FS_WORK = ["F0 convert+DFT (frame start)", "F0 row stores", "F1 reads+twiddle+DF
            "F2 reads+DFT, split, I0 DFT", "I0 row stores (+ queue)", "I1 reads+twiddle+DFT (+ prefetch)",
            "I1 row stores", "-", "-", "-", "-", "I2 reads+twiddle+DFT+emit (frame end)"]
 P_WORK = {
-    # d = 3 (N = 512): split to LDS, three radix-8 passes on wave 0
+    # d = 3 (N = 512): split + radix-2 step to LDS, the two 256-point halves on waves 0 and 1
     3: ["F0 convert+DFT (+ prefetch)", "F0 row stores", "F1 reads+twiddle+DFT", "F1 row stores",
-        "F2 reads+twiddle+DFT", "Z stores (+ queue)", "split x filter (Z reads, P/Q loads)", "filtered bins to LDS",
-        "-", "-", "-", "-", "wave-0 inverse tail + emit (frame end)"],
+        "F2 reads+twiddle+DFT", "Z stores (+ queue)", "split x filter (Z reads, P/Q loads)", "radix-2 halves to LDS",
+        "-", "-", "-", "-", "waves 0-1 inverse halves + emit (frame end)"],
     # d >= 4 (N <= 256): one filtered bin per thread to sb, wave-0 Stockham tail
     4: ["F0 convert+DFT (+ prefetch)", "F0 row stores", "F1 reads+twiddle+DFT", "F1 row stores",
         "F2 reads+twiddle+DFT", "Z stores (+ queue)", "split x filter to sb", "-", "-", "-", "-", "-",
