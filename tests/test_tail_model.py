@@ -72,3 +72,27 @@ def test_quad_first_pass(N):
         for h in range(per):
             got[per * t + h] = y[per * q + h]   # slot R j + r = per t + h
     assert np.abs(got - ref).max() < 1e-12
+
+
+def test_d3_two_half_tail():
+    """d = 3 (ddc_persistent.hip, tail_emit_half): the 512-point inverse as a radix-2 step in the
+    split's registers (E_p[m] = (X[m] + (-1)^p X[m + 256]) e^{2 pi i m p / 512}, m < 256), the d = 4
+    Stockham tail (4-4-4-4, layout tail_swz<256>) on each half, and half p's output y'[n'] placed
+    at n = 2 n' + p; the kept range of frame k (y[0, 384) for k >= 1, y[128, 384) for k = 0) is
+    what the two waves store (u[r] = y'[t + 64 r], r < 3, r >= 1 at k = 0)."""
+    rng = np.random.default_rng(512)
+    x = rng.standard_normal(512) + 1j * rng.standard_normal(512)
+    m = np.arange(256)
+    # the kernel's twiddle: TW<+1>(v, W_4096^{8m}) = v * conj(e^{-2 pi i 8 m / 4096})
+    w = np.conj(np.exp(-2j * np.pi * 8 * m / 4096))
+    halves = [x[:256] + x[256:], (x[:256] - x[256:]) * w]
+    y = np.zeros(512, complex)
+    for p, e in enumerate(halves):
+        yh = M.stockham_inv(e, 256, TAIL_SWZ[256])
+        y[2 * np.arange(256) + p] = yh
+    ref = np.fft.ifft(x) * 512
+    assert np.abs(y - ref).max() / np.abs(ref).max() < 1e-12
+    # the stores: lane t of wave p writes u[r] = y'[t + 64 r] at element 2 t + p + 128 r
+    for k, rs in ((0, (1, 2)), (1, (0, 1, 2))):
+        kept = sorted(2 * (t + 64 * r) + p for p in (0, 1) for t in range(64) for r in rs)
+        assert kept == list(range(128 if k == 0 else 0, 384))
