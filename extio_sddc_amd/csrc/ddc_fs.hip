@@ -145,11 +145,11 @@ template <> struct SchedOf<kSchedStatic> { using T = StaticSchedule; };
 template <> struct SchedOf<kSchedQueue> { using T = FrameSchedule<1>; };
 
 // ZR: whole rows of the inverse input known zero for this tune bin (the reference's zero fill,
-// impl.hpp:91-96): 4 = rows 12..15 (bins 3072..4095, tb <= 1024), -4 = rows 0..3 (bins 0..1023,
-// tb >= 3072), 0 = none.  Their (P, Q) loads and split FMAs are skipped and I0's first radix-4s
-// take only the live rows (dft16z).
+// impl.hpp:91-96; fs_zero_rows): ZR > 0 = rows 16 - ZR .. 15, ZR < 0 = rows 0 .. -ZR - 1, 4, 6
+// or 8 rows (tb = 1024, the benchmark's: rows 12..15).  Their (P, Q) loads and split FMAs
+// are skipped and I0's first radix-4s take only the live rows (dft16z).
 template <int ZR>
-__device__ __forceinline__ constexpr bool zrow(int k) { return ZR > 0 ? k >= 16 - ZR : ZR < 0 ? k < -ZR : false; }
+__device__ __forceinline__ constexpr bool zrow(int k) { return zr_row<ZR>(k); }
 
 template <int SCHED, int ZR, bool RAND, bool LSB, bool NCO, bool CS16>
 __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
@@ -484,9 +484,18 @@ hipError_t launch_fs_s(const KernelTables &t, const int16_t *d_in, int nblk, voi
     return hipGetLastError();
 }
 
-// zero rows of the inverse input for tune bin tb (ZR of r2iq_fs_kernel): 4 when bins 3072..4095 are
-// out of band (tb <= 1024), -4 when bins 0..1023 are (tb >= 3072), else 0
-int fs_zero_rows(int tunebin) { return tunebin <= 1024 ? 4 : tunebin >= 3072 ? -4 : 0; }
+// zero rows of the inverse input for tune bin tb (ZR of r2iq_fs_kernel): the band is
+// [tb - 2048, tb + 2048) clipped to [0, 4096) (the reference's zero fill, impl.hpp:91-96), so rows
+// k >= ceil((tb + 2048) / 256) are zero (tb < 2048, ZR > 0) or rows k < floor((tb - 2048) / 256)
+// (tb > 2048, ZR < 0); rounded down to 8, 6, 4 or none (the kernel's instances: with 2 zero rows
+// the compiler's schedule of the split's (P, Q) prefetch spills 256 VGPRs)
+int fs_zero_rows(int tunebin)
+{
+    const int top = 16 - (tunebin + 2048 + 255) / 256, bot = tunebin > 2048 ? (tunebin - 2048) / 256 : 0;
+    int z = top > 0 ? top : bot > 0 ? -bot : 0;
+    z = z > 8 ? 8 : z < -8 ? -8 : z / 2 * 2;
+    return z == 2 || z == -2 ? 0 : z;
+}
 
 template <int ZR, bool RAND, bool LSB, bool NCO, bool CS16>
 hipError_t launch_fs_z(const KernelTables &t, const int16_t *d_in, int nblk, void *d_out, const float4 *pqf,
@@ -495,7 +504,7 @@ hipError_t launch_fs_z(const KernelTables &t, const int16_t *d_in, int nblk, voi
 {
     if (fs.sched == kSchedStatic)
         return launch_fs_s<kSchedStatic, ZR, RAND, LSB, NCO, CS16>(t, d_in, nblk, d_out, pqf, fsl, tunebin, oa, nco, wq, fs, device, s);
-    if constexpr (!RAND && !LSB && !NCO && !CS16) {
+    if constexpr (!RAND && !LSB && !NCO && !CS16 && ZR % 4 == 0) {
         if (fs.sched == kSchedSteal)
             return launch_fs_s<kSchedSteal, ZR, false, false, false, false>(t, d_in, nblk, d_out, pqf, fsl, tunebin, oa, nco, wq, fs, device, s);
         if (fs.sched == kSchedQueue)
@@ -512,11 +521,12 @@ hipError_t launch_fs_v(const KernelTables &t, const int16_t *d_in, int nblk, voi
                        const float2 *fsl, int tunebin, const OutArgs &oa, const NcoArgs &nco, unsigned *wq,
                        const FsSched &fs, int device, hipStream_t s)
 {
-    const int zr = fs.zr ? fs_zero_rows(tunebin) : 0;
-    if (zr == 4)
-        return launch_fs_z<4, RAND, LSB, NCO, CS16>(t, d_in, nblk, d_out, pqf, fsl, tunebin, oa, nco, wq, fs, device, s);
-    if (zr == -4)
-        return launch_fs_z<-4, RAND, LSB, NCO, CS16>(t, d_in, nblk, d_out, pqf, fsl, tunebin, oa, nco, wq, fs, device, s);
+    int zr = fs.zr ? fs_zero_rows(tunebin) : 0;
+    if (fs.sched != kSchedStatic) zr = zr / 4 * 4;   // the A/B schedules: 0, +-4, +-8 only
+#define SDDC_FS_ZR(z) \
+    if (zr == (z)) return launch_fs_z<(z), RAND, LSB, NCO, CS16>(t, d_in, nblk, d_out, pqf, fsl, tunebin, oa, nco, wq, fs, device, s);
+    SDDC_FS_ZR(8) SDDC_FS_ZR(6) SDDC_FS_ZR(4) SDDC_FS_ZR(-4) SDDC_FS_ZR(-6) SDDC_FS_ZR(-8)
+#undef SDDC_FS_ZR
     return launch_fs_z<0, RAND, LSB, NCO, CS16>(t, d_in, nblk, d_out, pqf, fsl, tunebin, oa, nco, wq, fs, device, s);
 }
 

@@ -165,38 +165,52 @@ __device__ __forceinline__ void dft16(const float2 *v, float2 *o)
 }
 
 // dft16 with inputs known to be zero: ZR > 0: v[16 - ZR .. 15], ZR < 0: v[0 .. -ZR - 1]
-// (|ZR| = 4 or 8: whole inputs of every first-stage radix-4, n = 4 n1 + n2 with n1 = 3, or n1 = 2, 3,
-// or n1 = 0, or n1 = 0, 1).  Those radix-4s take their sums and differences from the live inputs
-// alone (x + 0 is not folded by the compiler: signed zeros), and the rest is dft16's; the outputs
-// equal dft16's on the same values exactly (the zero terms add nothing).
+// (|ZR| <= 8: in every first-stage radix-4 over n = 4 n1 + n2 at most one input of each
+// sum/difference pair (n1, n1 + 2) is zero).  Those radix-4s take their sums and differences from
+// the live inputs alone (x + 0 is not folded by the compiler: signed zeros), and the rest is
+// dft16's; the outputs equal dft16's on the same values (the zero terms add nothing).
+template <int ZR> __host__ __device__ constexpr bool zr_row(int k) { return ZR > 0 ? k >= 16 - ZR : ZR < 0 ? k < -ZR : false; }
+template <bool ZA, bool ZB> __device__ __forceinline__ float2 zsum(float2 a, float2 b)
+{
+    static_assert(!(ZA && ZB), "one zero per pair");
+    if constexpr (ZA) return b;
+    else if constexpr (ZB) return a;
+    else return cadd(a, b);
+}
+template <bool ZA, bool ZB> __device__ __forceinline__ float2 zdif(float2 a, float2 b)
+{
+    static_assert(!(ZA && ZB), "one zero per pair");
+    if constexpr (ZA) return make_float2(-b.x, -b.y);
+    else if constexpr (ZB) return a;
+    else return csub(a, b);
+}
+// the first-stage radix-4 of dft16z for inputs n2, 4 + n2, 8 + n2, 12 + n2
+template <int DIR, int ZR, int N2>
+__device__ __forceinline__ void dft16z_first(const float2 *v, float2 (&b)[4][4])
+{
+    constexpr bool z0 = zr_row<ZR>(N2), z1 = zr_row<ZR>(4 + N2), z2 = zr_row<ZR>(8 + N2), z3 = zr_row<ZR>(12 + N2);
+    const float2 a0 = v[N2], a1 = v[4 + N2], a2 = v[8 + N2], a3 = v[12 + N2];
+    const float2 t0 = zsum<z0, z2>(a0, a2), t1 = zdif<z0, z2>(a0, a2);
+    const float2 t2 = zsum<z1, z3>(a1, a3), t3 = mulj<DIR>(zdif<z1, z3>(a1, a3));
+    b[N2][0] = cadd(t0, t2);
+    b[N2][2] = csub(t0, t2);
+    b[N2][1] = cadd(t1, t3);
+    b[N2][3] = csub(t1, t3);
+}
 template <int DIR, int ZR>
 __device__ __forceinline__ void dft16z(const float2 *v, float2 *o)
 {
-    static_assert(ZR == 0 || ZR == 4 || ZR == -4 || ZR == 8 || ZR == -8, "zero rows: 0, +-4, +-8");
+    static_assert(ZR >= -8 && ZR <= 8, "zero rows: at most 8 at either end");
     if constexpr (ZR == 0) {
         dft16<DIR>(v, o);
     } else {
         constexpr float kT1 = 0.41421356237309504880f;
         constexpr float kT3 = 2.41421356237309504880f;
         float2 b[4][4];  // b[n2][k1]
-#pragma unroll
-        for (int n2 = 0; n2 < 4; n2++) {
-            const float2 a0 = v[n2], a1 = v[4 + n2], a2 = v[8 + n2], a3 = v[12 + n2];
-            float2 t0, t1, t2, t3;
-            if constexpr (ZR == 4) {   // a3 = 0
-                t0 = cadd(a0, a2), t1 = csub(a0, a2), t2 = a1, t3 = mulj<DIR>(a1);
-            } else if constexpr (ZR == 8) {   // a2 = a3 = 0
-                t0 = a0, t1 = a0, t2 = a1, t3 = mulj<DIR>(a1);
-            } else if constexpr (ZR == -4) {   // a0 = 0
-                t0 = a2, t1 = make_float2(-a2.x, -a2.y), t2 = cadd(a1, a3), t3 = mulj<DIR>(csub(a1, a3));
-            } else {   // a0 = a1 = 0
-                t0 = a2, t1 = make_float2(-a2.x, -a2.y), t2 = a3, t3 = mulj<DIR>(make_float2(-a3.x, -a3.y));
-            }
-            b[n2][0] = cadd(t0, t2);
-            b[n2][2] = csub(t0, t2);
-            b[n2][1] = cadd(t1, t3);
-            b[n2][3] = csub(t1, t3);
-        }
+        dft16z_first<DIR, ZR, 0>(v, b);
+        dft16z_first<DIR, ZR, 1>(v, b);
+        dft16z_first<DIR, ZR, 2>(v, b);
+        dft16z_first<DIR, ZR, 3>(v, b);
         dft4<DIR>(b[0][0], b[1][0], b[2][0], b[3][0], o[0], o[4], o[8], o[12]);
         float2 t0, t1, p, q;
         {   // k1 = 1 (as dft16)
