@@ -36,6 +36,8 @@
 // + lane offset), nt IQ stores.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "ddc_frame_common.hpp"
 #include "ddc_queue.hpp"
 #include "ddc_stamps.hpp"
@@ -200,10 +202,29 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
     const int col_ = kFsPerm[tid];
     const int qt = (tunebin >> 2) & 3;   // (tb mod 16) / 4: the output quarter turns
     const bool w0 = __builtin_amdgcn_readfirstlane(tid >> 6) == 0;   // the wave holding columns 0, 128
+    // The frame loop runs in two phases.  Phase A: frames of the workgroup's own range whose next
+    // frame and the one after it are private too (StaticSchedule: all of them), the next frame
+    // f + 1, known to every wave, no schedule state.  Phase B: the rest, with the schedule object
+    // on the queue wave and the next frame through s_next (the queue: every frame; work stealing:
+    // the range's public end and what it steals).  Phase A is a copy of the frame body without
+    // the schedule's registers, so the owner's frames cost what the static schedule's do.
+    int pA = -1, fend = -1;
+    {
+        const int G = (int)gridDim.x, a = slot_split(ns, G, w, slotw), b = slot_split(ns, G, w + 1, slotw);
+        if constexpr (SCHED == kSchedStatic) {
+            pA = b + 2;
+            fend = b;
+        } else if constexpr (SCHED == kSchedSteal) {
+            const int len = b - a, two = len < 2 ? len : 2;
+            pA = minrem <= 0 ? b + 2 : a + (pub > 0 && len - pub > two ? len - pub : two);
+            fend = minrem <= 0 ? b : pA;
+        }
+    }
     ST_INIT();
 
-    while (f >= 0) {
-        if constexpr (SCHED != kSchedSteal)
+    auto frame = [&](auto phase) __attribute__((always_inline)) {
+        constexpr bool PB = decltype(phase)::value;
+        if constexpr (PB && SCHED != kSchedSteal)
             if (qw) fsch.peek();
         // opaque per-frame copies of the thread index and column: without them the compiler
         // hoists every loop-invariant LDS address out of the frame loop and spills them
@@ -255,7 +276,7 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
             for (int r = 0; r < 16; r++) col[272 * r + (r >= 8)] = v[r];
         }
         ST_SYNC(3);
-        if constexpr (SCHED == kSchedSteal)
+        if constexpr (PB && SCHED == kSchedSteal)
             if (qw) fsch.peek();
         // ---- F2 (R16, NS256) on column c: Z[c + 256 k] in v[k] ----
         // The split's (P, Q) loads (bin pairs p, 15 - p) run a pair ahead of their use, the first
@@ -343,10 +364,13 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
 #pragma unroll
             for (int r = 0; r < 16; r++) cb[17 * r] = u[r];
         }
-        // the next frame (static, or the ticket read at this frame's top; ddc_queue.hpp)
-        if (qw) {
-            const int f_n = fsch.next();
-            if (tid == QLANE) s_next = f_n;
+        // the next frame (phase B: the schedule's, from the ticket read at this frame's top;
+        // ddc_queue.hpp)
+        if constexpr (PB) {
+            if (qw) {
+                const int f_n = fsch.next();
+                if (tid == QLANE) s_next = f_n;
+            }
         }
         ST_SYNC(5);
         // I2's lane factors g_t, g_t W^{-t}, g_t W^{-4t} (exactly rounded, from the per-tunebin
@@ -367,7 +391,8 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
             // the next frame's number is read behind the data reads (its LDS round trip under
             // theirs), and its input loads are issued here rather than in F0, so their 16
             // registers are free through F2 and the split
-            fn = s_next;
+            if constexpr (PB) fn = s_next;
+            else fn = f + 1 < fend ? f + 1 : -1;
             if (fn >= 0) {
                 blk = fn / FRAMES;
                 k = fn - blk * FRAMES;
@@ -376,7 +401,8 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
             // the ticket for the frame after the next one, when that one is dynamic: behind this
             // frame's last loads (vmcnt counts in issue order: taken at inverse pass 0, the wait
             // for I2's lane factors included the atomic); read at the next frame's top
-            if (qw) fsch.take();
+            if constexpr (PB)
+                if (qw) fsch.take();
             table_twiddle<+1, true>(a, twl, 16, x15);
             dft16<+1>(a, u);
         }
@@ -410,10 +436,19 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
             default: emit_frame_q<3, LSB, NCO, CS16>(out, fb, kc, t, u, oa, nco); break;
             }
         }
-        if constexpr (SCHED == kSchedSteal)
-            if (qw) fsch.take_late();
+        if constexpr (SCHED == kSchedSteal) {
+            if constexpr (PB)
+                if (qw) fsch.take_late();
+        }
         ST_FRAME_END();
         f = fn;
+    };
+    if constexpr (SCHED != kSchedQueue)
+        while (f >= 0 && f + 2 < pA) frame(std::false_type{});
+    if constexpr (SCHED != kSchedStatic) {
+        if constexpr (SCHED == kSchedSteal)
+            if (qw) fsch.enter(f);
+        while (f >= 0) frame(std::true_type{});
     }
     ST_WRITE(g_fs_stamps, w, tid);
     if constexpr (SCHED == kSchedQueue)

@@ -325,7 +325,15 @@ struct StealSchedule {
             (void)atomicExch(reinterpret_cast<unsigned long long *>(slots) + w, v);
         }
         if (len <= 0) mode = kDone;   // nothing of its own (a tiny batch)
-        else take_late();             // a one-frame range steals from its first frame on
+    }
+    // phase B of the frame loop (ddc_fs.hip) starts at frame f, the private frames before it done
+    // without this object: the state of the end of frame f - 1, and its scan (a one- or two-frame
+    // range steals from its first frame on)
+    __device__ __forceinline__ void enter(int f)
+    {
+        if (f < 0) return;
+        nx = f + 1;
+        take_late();
     }
     __device__ __forceinline__ void peek()
     {
