@@ -554,11 +554,18 @@ hipError_t launch_fs_v(const KernelTables &t, const int16_t *d_in, int nblk, voi
                        const float2 *fsl, int tunebin, const OutArgs &oa, const NcoArgs &nco, unsigned *wq,
                        const FsSched &fs, int device, hipStream_t s)
 {
+    // every even zero-row count for the CF32 outputs without NCO; the fused-NCO and CS16 outputs
+    // (and the A/B schedules) take 0 or 4 (fewer instances: the file compiles in parallel with
+    // nothing, and each count is a whole kernel per output configuration)
+    constexpr bool FINE = !NCO && !CS16;
     int zr = fs.zr ? fs_zero_rows(tunebin) : 0;
-    if (fs.sched != kSchedStatic) zr = zr / 4 * 4;   // the A/B schedules: 0, +-4, +-8 only
+    if (!FINE || fs.sched != kSchedStatic) zr = zr >= 4 ? 4 : zr <= -4 ? -4 : 0;
 #define SDDC_FS_ZR(z) \
     if (zr == (z)) return launch_fs_z<(z), RAND, LSB, NCO, CS16>(t, d_in, nblk, d_out, pqf, fsl, tunebin, oa, nco, wq, fs, device, s);
-    SDDC_FS_ZR(8) SDDC_FS_ZR(6) SDDC_FS_ZR(4) SDDC_FS_ZR(2) SDDC_FS_ZR(-2) SDDC_FS_ZR(-4) SDDC_FS_ZR(-6) SDDC_FS_ZR(-8)
+    SDDC_FS_ZR(4) SDDC_FS_ZR(-4)
+    if constexpr (FINE) {
+        SDDC_FS_ZR(8) SDDC_FS_ZR(6) SDDC_FS_ZR(2) SDDC_FS_ZR(-2) SDDC_FS_ZR(-6) SDDC_FS_ZR(-8)
+    }
 #undef SDDC_FS_ZR
     return launch_fs_z<0, RAND, LSB, NCO, CS16>(t, d_in, nblk, d_out, pqf, fsl, tunebin, oa, nco, wq, fs, device, s);
 }
