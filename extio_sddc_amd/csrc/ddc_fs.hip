@@ -147,8 +147,8 @@ template <> struct SchedOf<kSchedStatic> { using T = StaticSchedule; };
 template <> struct SchedOf<kSchedQueue> { using T = FrameSchedule<1>; };
 
 // ZR: whole rows of the inverse input known zero for this tune bin (the reference's zero fill,
-// impl.hpp:91-96; fs_zero_rows): ZR > 0 = rows 16 - ZR .. 15, ZR < 0 = rows 0 .. -ZR - 1, 2, 4,
-// 6 or 8 rows (tb = 1024, the benchmark's: rows 12..15).  Their (P, Q) loads and split FMAs
+// impl.hpp:91-96; fs_zero_rows): ZR > 0 = rows 16 - ZR .. 15, ZR < 0 = rows 0 .. -ZR - 1, 2 to 8
+// rows (tb = 1024, the benchmark's: rows 12..15).  Their (P, Q) loads and split FMAs
 // are skipped and I0's first radix-4s take only the live rows (dft16z).
 template <int ZR>
 __device__ __forceinline__ constexpr bool zrow(int k) { return zr_row<ZR>(k); }
@@ -522,12 +522,13 @@ hipError_t launch_fs_s(const KernelTables &t, const int16_t *d_in, int nblk, voi
 // zero rows of the inverse input for tune bin tb (ZR of r2iq_fs_kernel): the band is
 // [tb - 2048, tb + 2048) clipped to [0, 4096) (the reference's zero fill, impl.hpp:91-96), so rows
 // k >= ceil((tb + 2048) / 256) are zero (tb < 2048, ZR > 0) or rows k < floor((tb - 2048) / 256)
-// (tb > 2048, ZR < 0); rounded down to an even count (the kernel's instances: 2, 4, 6, 8)
+// (tb > 2048, ZR < 0), at most 8 (dft16z); a single zero row runs unskipped (with it the
+// compiler's schedule of the (P, Q) prefetch spills 5-6 VGPRs)
 int fs_zero_rows(int tunebin)
 {
     const int top = 16 - (tunebin + 2048 + 255) / 256, bot = tunebin > 2048 ? (tunebin - 2048) / 256 : 0;
     const int z = top > 0 ? top : bot > 0 ? -bot : 0;
-    return z > 8 ? 8 : z < -8 ? -8 : z / 2 * 2;
+    return z > 8 ? 8 : z < -8 ? -8 : z == 1 || z == -1 ? 0 : z;
 }
 
 template <int ZR, bool RAND, bool LSB, bool NCO, bool CS16>
@@ -554,9 +555,9 @@ hipError_t launch_fs_v(const KernelTables &t, const int16_t *d_in, int nblk, voi
                        const float2 *fsl, int tunebin, const OutArgs &oa, const NcoArgs &nco, unsigned *wq,
                        const FsSched &fs, int device, hipStream_t s)
 {
-    // every even zero-row count for the CF32 outputs without NCO; the fused-NCO and CS16 outputs
-    // (and the A/B schedules) take 0 or 4 (fewer instances: the file compiles in parallel with
-    // nothing, and each count is a whole kernel per output configuration)
+    // every zero-row count for the CF32 outputs without NCO; the fused-NCO and CS16 outputs (and
+    // the A/B schedules) take 0 or 4 (fewer instances: the file compiles in parallel with nothing,
+    // and each count is a whole kernel per output configuration)
     constexpr bool FINE = !NCO && !CS16;
     int zr = fs.zr ? fs_zero_rows(tunebin) : 0;
     if (!FINE || fs.sched != kSchedStatic) zr = zr >= 4 ? 4 : zr <= -4 ? -4 : 0;
@@ -564,7 +565,8 @@ hipError_t launch_fs_v(const KernelTables &t, const int16_t *d_in, int nblk, voi
     if (zr == (z)) return launch_fs_z<(z), RAND, LSB, NCO, CS16>(t, d_in, nblk, d_out, pqf, fsl, tunebin, oa, nco, wq, fs, device, s);
     SDDC_FS_ZR(4) SDDC_FS_ZR(-4)
     if constexpr (FINE) {
-        SDDC_FS_ZR(8) SDDC_FS_ZR(6) SDDC_FS_ZR(2) SDDC_FS_ZR(-2) SDDC_FS_ZR(-6) SDDC_FS_ZR(-8)
+        SDDC_FS_ZR(8) SDDC_FS_ZR(7) SDDC_FS_ZR(6) SDDC_FS_ZR(5) SDDC_FS_ZR(3) SDDC_FS_ZR(2)
+        SDDC_FS_ZR(-2) SDDC_FS_ZR(-3) SDDC_FS_ZR(-5) SDDC_FS_ZR(-6) SDDC_FS_ZR(-7) SDDC_FS_ZR(-8)
     }
 #undef SDDC_FS_ZR
     return launch_fs_z<0, RAND, LSB, NCO, CS16>(t, d_in, nblk, d_out, pqf, fsl, tunebin, oa, nco, wq, fs, device, s);
