@@ -61,6 +61,33 @@ def make_input(torch, nblk: int, seed: int, device, first_block: int = 0) -> "to
     return out
 
 
+def segment_check(torch, ddc, d: int, nblk: int, rank: int, dev, stream, d_out) -> dict:
+    """Time-segment self-check: this rank's launch output d_out (blocks
+    [rank nblk, (rank + 1) nblk) of the one stream, with its 4096-sample halo from the previous
+    rank's segment) against an independent launch of the same kernel over a 2-block window that
+    starts one block earlier.  The window's second block must equal the segment's block bit for
+    bit: its history then comes from the window's own first block, i.e. the previous rank's data
+    for the segment's first block (rank > 0), so a wrong halo shows.  Checked: the segment's first
+    block (rank > 0) and its middle block (every rank).  GPU against GPU (the oracle stays in the
+    cpu_baseline leg)."""
+    from extio_sddc_amd import output_samples
+    per = output_samples(d, 1) * 2                      # floats of one block's output
+    first = rank * nblk
+    blocks = ([first] if rank > 0 else []) + [first + nblk // 2]
+    worst, identical = 0.0, True
+    for b in blocks:
+        win = make_input(torch, 2, 0x5DDC, dev, first_block=b - 1)
+        wout = torch.empty(2 * per, dtype=d_out.dtype, device=dev)
+        ddc.process_device(win, 2, wout, stream)
+        torch.cuda.synchronize()
+        seg = d_out[(b - first) * per:(b - first + 1) * per].double()
+        ref = wout[per:].double()
+        worst = max(worst, ((seg - ref).abs().max() / ref.abs().max()).item())
+        identical = identical and bool(torch.equal(d_out[(b - first) * per:(b - first + 1) * per], wout[per:]))
+        del win, wout
+    return {"blocks_checked": blocks, "max_rel_err": worst, "bit_identical": identical}
+
+
 def _cpu_model() -> str:
     try:
         for line in subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout.splitlines():
@@ -664,6 +691,18 @@ def main() -> None:
                           "launch duration, from the same steps on one stream"}
         kern_ms = kern1
 
+    # single mode: every rank checks its segment (the halo'd first block, a middle block) against
+    # a separate launch over a window starting a block earlier; max error / all identical over ranks
+    seg_check = None
+    if args.mode == "single" and not (args.cs16 or args.fine_tune):
+        seg_check = segment_check(torch, ddc, d, nblk, rank, dev, stream, pouts[0])
+        if world > 1:
+            tt = torch.tensor([seg_check["max_rel_err"], 0.0 if seg_check["bit_identical"] else 1.0],
+                              dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            seg_check = {"ranks": world, "blocks_checked_rank0": seg_check["blocks_checked"],
+                         "max_rel_err_over_ranks": tt[0].item(), "bit_identical_all_ranks": tt[1].item() == 0.0}
+
     # N > 1 channels: the collective and the compute, each timed alone (max over ranks), so the
     # line shows which of the two bounds the pipelined step
     bcast_info = None
@@ -737,6 +776,8 @@ def main() -> None:
         result["broadcast"] = bcast_info
     if args.mode == "channels" and world > 1:
         result["broadcast_check"] = ch.bcast_check
+    if seg_check:
+        result["segment_check"] = seg_check
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         ns = 16
         sample = d_in[: HALF + ns * BLOCK].cpu().numpy()

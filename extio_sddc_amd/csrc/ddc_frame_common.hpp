@@ -1,6 +1,5 @@
 // ddc_frame_common.hpp — device helpers shared by the single-channel frame kernels: the
-// default persistent kernel (ddc_persistent.hip) and the d = 0 A/B variants built into
-// libsddc_ddc_variants.so (variants/ddc_variants.hip).
+// persistent kernel (ddc_persistent.hip, d >= 1) and the d = 0 fused-split kernel (ddc_fs.hip).
 //
 // Frame k of input block b is the 8192 samples at 65536 b + 6144 k of the batch's
 // [history 4096 | blocks] buffer (Core/fft_mt_r2iq_impl.hpp:84-88); one 256-thread

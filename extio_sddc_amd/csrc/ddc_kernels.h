@@ -1,5 +1,6 @@
 // ddc_kernels.h — internal (C++) interface between the runtime and the HIP kernels of the
-// product library.  The A/B variant kernels live in libsddc_ddc_variants.so (variants/).
+// product library.  (The measured-slower A/B kernels of rounds 1-5 are in git history; DESIGN.md
+// §8 keeps their numbers.)
 #pragma once
 
 #include <hip/hip_runtime_api.h>
@@ -60,8 +61,6 @@ struct KernelTables {
     const float2 *tw_q1[7] = {};       // [15][S]:  W_{16S}^{s r}   inverse pass 1, S = NS of that pass
     const float2 *rec_f = nullptr;     // [2][256]: W_4096^{j}, W_4096^{4j}  forward pass 2 recurrence
     const float2 *rec_i[7] = {};       // [2][256]: W_N^{j}, W_N^{4j}        inverse pass 2 (N >= 512)
-    const float2 *twf64 = nullptr;     // [64][64]: W_4096^{L q} at [q][L]  wave kernel F1 twiddles (d = 0,
-                                       // libsddc_ddc_variants.so)
     LaunchCache *lc = nullptr;         // the handle's launch geometry (written under the handle's lock)
 };
 

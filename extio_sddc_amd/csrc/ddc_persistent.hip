@@ -16,8 +16,8 @@
 //   * twiddles: small [r][s] tables copied to LDS once per workgroup for the NS <= 16 passes,
 //     a register recurrence from per-thread W^j, W^{4j} for the NS = 256 passes; the r2c split
 //     twiddle and the filter are one (P, Q) float4 per inverse input (build_split_filter_kernel).
-// The measured-slower layouts and the first-generation kernels are in variants/ (built into
-// libsddc_ddc_variants.so); the timing-only builds of the A/B study are in git history.
+// The measured-slower layouts, the first-generation kernels and the timing-only builds of the
+// A/B study are in git history (DESIGN.md §8 keeps their numbers).
 #include <hip/hip_runtime.h>
 
 #include "ddc_frame_common.hpp"

@@ -237,13 +237,16 @@ struct StealSchedule {
     int va;         // the pending steal's victim range start
     int lim;        // frames of the launch (no claim returns a frame past it)
     int minrem;     // steal only from ranges with at least this many unclaimed frames
+    int self;       // this workgroup's range (and steal slot) index: blockIdx.x, or the XCD-mapped
+                    // index of a non-persistent grid (ddc_fs.hip xmap); every slot access uses it
 
-    // this lane's scan candidate of probe k (byte offset of its slot): 64 slots spread over XCDs
-    // (blockIdx % 8) and CU slots (blockIdx / (G / 4)); stride S odd and > G / 64 for G >= 128, so
-    // the 64 are distinct and not w; lanes past G - 1 candidates are out of the buffer (dropped)
+    // this lane's scan candidate of probe k (byte offset of its slot): 64 slots spread over the
+    // range indices (persistent grids: XCDs = index % 8, CU slots = index / (G / 4)); stride S odd
+    // and > G / 64 for G >= 128, so the 64 are distinct and not self; lanes past G - 1 candidates
+    // are out of the buffer (dropped)
     __device__ __forceinline__ unsigned cand_off(int k) const
     {
-        const int G = (int)gridDim.x, w = (int)blockIdx.x;
+        const int G = (int)gridDim.x, w = self;
         const int l = (int)(threadIdx.x & 63);
         if (l >= G - 1) return STEAL_OOB;
         const int S = G >= 128 ? (G >> 6) + 1 : 1;
@@ -254,7 +257,7 @@ struct StealSchedule {
     }
     __device__ __forceinline__ void claim_own()
     {
-        const unsigned voff = (threadIdx.x & 63) == 0 ? 8u * blockIdx.x : STEAL_OOB;
+        const unsigned voff = (threadIdx.x & 63) == 0 ? 8u * (unsigned)self : STEAL_OOB;
         tk = __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(0x10000, rs, voff, 0, 0);
         mode = kOwn;
     }
@@ -303,6 +306,7 @@ struct StealSchedule {
         rs = __builtin_amdgcn_make_buffer_rsrc(slots, (short)0, 8 * G, 0x00020000);
         lim = nframes;
         minrem = minrem_;
+        self = w;
         a = slot_split(ns, G, w, slotw);
         const int len = slot_split(ns, G, w + 1, slotw) - a;
         f[0] = len > 0 ? a : -1;

@@ -5,7 +5,6 @@
 // (here: twiddle tables), the tune bin and the stream history.  A GPU handle's compute
 // calls go to the gfx950 kernels only (no fallback); a handle created on
 // SDDC_DDC_DEVICE_CPU holds the AVX2 backend (cpu/r2iq_cpu.h) instead and never calls HIP.
-#include <dlfcn.h>
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
@@ -28,7 +27,6 @@
 #include "sddc_fft.h"
 #include "sddc_ddc.h"
 #include "sddc_ddc_internal.h"
-#include "variants/variants_api.h"
 
 namespace {
 
@@ -133,48 +131,12 @@ struct Readers {
     }
 };
 
-// The A/B variant kernels (variants/variants_api.h) live in libsddc_ddc_variants.so next to
-// this library; it is loaded the first time a handle selects a variant.
-std::once_flag g_variants_once;
-const sddc_variants_api *g_variants = nullptr;
-std::string g_variants_err;
-
-const sddc_variants_api *variants()
-{
-    std::call_once(g_variants_once, [] {
-        std::string path = "libsddc_ddc_variants.so";
-        Dl_info info;
-        if (dladdr(reinterpret_cast<void *>(&sddc_ddc_abi_version), &info) && info.dli_fname) {
-            const std::string self = info.dli_fname;
-            const size_t slash = self.find_last_of('/');
-            if (slash != std::string::npos) path = self.substr(0, slash + 1) + path;
-        }
-        void *lib = dlopen(path.c_str(), RTLD_NOW | RTLD_LOCAL);
-        if (!lib) {
-            g_variants_err = dlerror();
-            return;
-        }
-        auto get = reinterpret_cast<const sddc_variants_api *(*)()>(dlsym(lib, "sddc_variants_get"));
-        const sddc_variants_api *api = get ? get() : nullptr;
-        if (!api || api->version != SDDC_VARIANTS_API_VERSION) {
-            g_variants_err = path + ": no sddc_variants_get of version " + std::to_string(SDDC_VARIANTS_API_VERSION);
-            return;
-        }
-        g_variants = api;
-    });
-    return g_variants;
-}
-
 }  // namespace
 
 struct sddc_ddc {
     int device = 0;
     float gain = 0.f;
     int d = 0, lsb = 0, rand = 0, tunebin = SDDC_DDC_HALF_FFT / 4;   // ctor: mtunebin = halfFft/4
-    int variant = 0;                       // 0: persistent (v2); 1: one workgroup per frame (v1);
-                                           // 3: one wave per frame at d = 0 (ddc_wave.hip), 4: two frames in
-                                           // flight per workgroup at d = 0, 5: radix 8 x 512 threads at
-                                           // d = 0; persistent otherwise
     int out_fmt = SDDC_DDC_FMT_CF32;       // output stage format
     float cs16_scale = 1.f;
     sddc::KernelTables tables;
@@ -209,16 +171,13 @@ struct sddc_ddc {
 
     // split x filter coefficients of the current (d, tunebin), rebuilt on device when either
     // changes; readers = the streams of single-channel launches that read them (and d_nco)
-    // Each table set remembers the stream its last rebuild ran on (pq_s, wave_s, fs_s): a launch
+    // Each table set remembers the stream its last rebuild ran on (pq_s, fs_s): a launch
     // on another stream first waits for that stream's last recorded launch (Readers::order_after),
     // which is behind the rebuild (a rebuild is recorded like a launch).
     float4 *d_pq = nullptr;
     int pq_d = -1, pq_tb = -1;
     hipStream_t pq_s = nullptr;
     // the d = 0 wave kernel's per-tunebin tables: pqW (4096 float4) then twI (4096 float2)
-    float4 *d_wave = nullptr;
-    int wave_tb = -1;
-    hipStream_t wave_s = nullptr;
     // the d = 0 fused-split kernel's per-tunebin tables: pqf (4096 float4) then fsl (768 float2)
     float4 *d_fs = nullptr;
     int fs_tb = -1;
@@ -377,9 +336,6 @@ int sddc_ddc_create(float gain, int device, sddc_ddc_t **out)
         host[o_recf + j] = W(j, 4096);
         host[o_recf + 256 + j] = W(4.0 * j, 4096);
     }
-    const size_t o_twf64 = put(64 * 64);   // wave kernel F1 twiddles W_4096^{L q} at [q][L]
-    for (int q = 0; q < 64; q++)
-        for (int L = 0; L < 64; L++) host[o_twf64 + 64 * q + L] = W((double)((L * q) & 4095), 4096);
     size_t o_hsel[SDDC_DDC_NDEC], o_q1[SDDC_DDC_NDEC], o_reci[SDDC_DDC_NDEC];
     std::vector<std::complex<double>> H(SDDC_DDC_HALF_FFT);
     for (int d = 0; d < SDDC_DDC_NDEC; d++) {
@@ -411,7 +367,6 @@ int sddc_ddc_create(float gain, int device, sddc_ddc_t **out)
     if (e == hipSuccess) e = hipMemcpy(h->d_tables, host.data(), ntab * sizeof(float2), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipMalloc(&h->d_pq, SDDC_DDC_HALF_FFT * sizeof(float4));
-    if (e == hipSuccess) e = hipMalloc(&h->d_wave, 4096 * (sizeof(float4) + sizeof(float2)));
     if (e == hipSuccess) e = hipMalloc(&h->d_fs, 4096 * sizeof(float4) + 768 * sizeof(float2));
     if (e == hipSuccess)
         e = hipMalloc(&h->d_queue, (size_t)sddc_ddc::kQueueSlots * sddc::kFsQueueWords * sizeof(unsigned));
@@ -428,7 +383,6 @@ int sddc_ddc_create(float gain, int device, sddc_ddc_t **out)
     h->tables.post8192 = T + o_post;
     h->tables.tw_p1 = T + o_p1;
     h->tables.rec_f = T + o_recf;
-    h->tables.twf64 = T + o_twf64;
     h->tables.lc = &h->launch_cache;
     for (int d = 0; d < SDDC_DDC_NDEC; d++) {
         h->tables.hsel[d] = T + o_hsel[d];
@@ -478,7 +432,6 @@ int sddc_ddc_destroy(sddc_ddc_t *h)
         if (h->d_windows) (void)hipFree(h->d_windows);
         if (h->d_chscratch) (void)hipFree(h->d_chscratch);
         if (h->d_pq) (void)hipFree(h->d_pq);
-        if (h->d_wave) (void)hipFree(h->d_wave);
         if (h->d_fs) (void)hipFree(h->d_fs);
         if (h->d_queue) (void)hipFree(h->d_queue);
         h->readers.clear();
@@ -674,42 +627,13 @@ static hipError_t launch_single(sddc_ddc_t *h, const int16_t *d_in, int nblk, vo
 
 static hipError_t launch_single_impl(sddc_ddc_t *h, const int16_t *d_in, int nblk, void *d_out, hipStream_t s)
 {
-    const sddc_variants_api *V = h->variant ? variants() : nullptr;   // set_variant checked it loads
-    if (h->variant == 1) {
-        // the v1 reference variant has neither the NCO nor the CS16 stage
-        if (h->nco_fc != 0.f || h->out_fmt != SDDC_DDC_FMT_CF32) return hipErrorNotSupported;
-        return V->frames_v1(h->tables, h->d, d_in, nblk, static_cast<float *>(d_out), h->tunebin, h->lsb, h->rand,
-                            s);
-    }
     const bool nco = h->nco_fc != 0.f;
     if (nco) {
         hipError_t e = stage_nco(h, nblk, s);
         if (e != hipSuccess) return e;
     }
-    if (h->d == 0 && h->variant == 3) {
-        // wave kernel (ddc_wave.hip): its (P, Q) and inverse twiddles in lane layout
-        float4 *pqW = h->d_wave;
-        float2 *twI = reinterpret_cast<float2 *>(h->d_wave + 4096);
-        if (h->wave_tb != h->tunebin) {
-            hipError_t e = h->readers.order_before(s);   // launches on other streams may still read them
-            if (e != hipSuccess) return e;
-            h->wave_tb = -1;
-            e = V->build_wave_tables(h->tables, h->tunebin, pqW, twI, s);
-            if (e == hipSuccess) e = h->readers.record(s);
-            if (e != hipSuccess) return e;
-            h->wave_tb = h->tunebin;
-            h->wave_s = s;
-        } else if (hipError_t e = order_after_build(h, h->wave_s, s); e != hipSuccess) {
-            return e;
-        }
-        hipError_t e = V->frames_wave(
-            h->tables, d_in, nblk, d_out, pqW, twI, h->tunebin, h->lsb, h->rand, h->out_fmt == SDDC_DDC_FMT_CS16,
-            h->cs16_scale, nco ? h->d_nco + sddc::FineTune::kTable : nullptr, nco ? h->d_nco : nullptr, h->device, s);
-        if (e != hipSuccess) return e;
-        return h->readers.record(s);
-    }
     const float2 *nco_starts = nco ? h->d_nco + sddc::FineTune::kTable : nullptr, *nco_trig = nco ? h->d_nco : nullptr;
-    if (h->variant == 0 && sddc::fs_path(h->d, h->tunebin)) {
+    if (sddc::fs_path(h->d, h->tunebin)) {
         // d = 0 fused-split kernel: its (P, Q) by bin and output-modulation lane factors
         float4 *pqf = h->d_fs;
         float2 *fsl = reinterpret_cast<float2 *>(h->d_fs + 4096);
@@ -751,20 +675,7 @@ static hipError_t launch_single_impl(sddc_ddc_t *h, const int16_t *d_in, int nbl
     } else if (hipError_t e = order_after_build(h, h->pq_s, s); e != hipSuccess) {
         return e;
     }
-    hipError_t e = h->d == 0 && h->variant == 7
-        ? V->frames_inplace(h->tables, d_in, nblk, d_out, h->d_pq, h->tunebin, h->lsb, h->rand,
-                            h->out_fmt == SDDC_DDC_FMT_CS16, h->cs16_scale, nco_starts, nco_trig, h->device, s)
-        : h->d == 0 && h->variant == 6
-        ? V->frames_pair(h->tables, d_in, nblk, d_out, h->d_pq, h->tunebin, h->lsb, h->rand,
-                         h->out_fmt == SDDC_DDC_FMT_CS16, h->cs16_scale, nco_starts, nco_trig, h->device, s)
-        : h->d == 0 && h->variant == 5
-        ? V->frames_r8(h->tables, d_in, nblk, d_out, h->d_pq, h->tunebin, h->lsb, h->rand,
-                                 h->out_fmt == SDDC_DDC_FMT_CS16, h->cs16_scale, nco_starts, nco_trig, h->device, s)
-        : h->d == 0 && h->variant == 4
-        ? V->frames_pipelined(h->tables, d_in, nblk, d_out, h->d_pq, h->tunebin, h->lsb, h->rand,
-                                        h->out_fmt == SDDC_DDC_FMT_CS16, h->cs16_scale, nco_starts, nco_trig,
-                                        h->device, s)
-        : sddc::launch_frames_persistent(h->tables, h->d, d_in, nblk, d_out, h->d_pq, h->tunebin, h->lsb, h->rand,
+    hipError_t e = sddc::launch_frames_persistent(h->tables, h->d, d_in, nblk, d_out, h->d_pq, h->tunebin, h->lsb, h->rand,
                                          h->out_fmt == SDDC_DDC_FMT_CS16, h->cs16_scale, nco_starts, nco_trig,
                                          h->slot_weights, h->device, s);
     if (e != hipSuccess) return e;
@@ -793,18 +704,6 @@ int sddc_ddc_set_fine_tune(sddc_ddc_t *h, float relative_freq)
         h->nco_fc = relative_freq;
         if (relative_freq != 0.f) h->nco.init(relative_freq, 0.0f);
     }
-    return SDDC_OK;
-}
-
-/* internal (not in include/sddc_ddc.h): kernel variant for A/B timing, see sddc_ddc_internal.h */
-int sddc_ddc_internal_set_variant(sddc_ddc_t *h, int variant)
-{
-    if (!h || variant < 0 || variant > 7 || variant == 2) return fail(SDDC_ERR_ARG, "bad variant");
-    if (h->cpu) return fail(SDDC_ERR_STATE, "kernel variants are GPU-only");
-    if (variant && !variants())
-        return fail(SDDC_ERR_STATE, "variant %d needs libsddc_ddc_variants.so: %s", variant, g_variants_err.c_str());
-    std::lock_guard<std::mutex> lk(h->mu);
-    h->variant = variant;
     return SDDC_OK;
 }
 
@@ -894,7 +793,7 @@ int sddc_ddc_process_channels_device(sddc_ddc_t *h, const int16_t *d_in, int nbl
     DeviceGuard g(h->device);
     HIP_TRY(g.err);
     hipStream_t s = (hipStream_t)hip_stream;
-    const bool v2 = h->d >= 4 && h->variant != 1;
+    const bool v2 = h->d >= 4;
     const bool changed = h->tunebins_cached.size() != (size_t)nch ||
                          !std::equal(h->tunebins_cached.begin(), h->tunebins_cached.end(), tunebins);
     if (changed || (v2 && h->windows_d != h->d && h->windows_d != -2 - 8 * h->d)) {
@@ -918,12 +817,12 @@ int sddc_ddc_process_channels_device(sddc_ddc_t *h, const int16_t *d_in, int nbl
                 HIP_TRY(hipMemcpy(h->d_windows, w.data(), w.size() * sizeof(int2), hipMemcpyHostToDevice));
                 h->windows_d = h->d;
             } else {
-                h->windows_d = -2 - 8 * h->d;   // spread-out tune bins: full-spectrum variant
+                h->windows_d = -2 - 8 * h->d;   // spread-out tune bins: the full-spectrum form
             }
         }
         if (h->windows_d == h->d) windows = h->d_windows;
     }
-    if (((v2 && windows && nch > 128) || !v2) && h->variant != 1 && !h->d_chscratch) {
+    if (((v2 && windows && nch > 128) || !v2) && !h->d_chscratch) {
         // one 4096-bin row per resident workgroup (<= 4 per CU), 32 KB each
         int cus = 0;
         HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, h->device));
@@ -936,13 +835,10 @@ int sddc_ddc_process_channels_device(sddc_ddc_t *h, const int16_t *d_in, int nbl
         HIP_TRY(sddc::launch_channels_v2(h->tables, h->d, d_in, nblk, h->d_tunebins, nch, d_out, out_stride,
                                          h->lsb, h->rand, cs16, h->cs16_scale, windows, h->d_chscratch,
                                          h->chscratch_rows, h->device, s));
-    else if (h->variant != 1)
+    else
         HIP_TRY(sddc::launch_channels_p(h->tables, h->d, d_in, nblk, h->d_tunebins, nch, d_out, out_stride,
                                         h->lsb, h->rand, cs16, h->cs16_scale, h->d_chscratch, h->chscratch_rows,
                                         h->device, s));
-    else
-        HIP_TRY(variants()->channels_v1(h->tables, h->d, d_in, nblk, h->d_tunebins, nch, d_out, out_stride,
-                                      h->lsb, h->rand, cs16, h->cs16_scale, s));
     HIP_TRY(h->ch_readers.record(s));
     return SDDC_OK;
 }

@@ -4,13 +4,6 @@
 #ifdef __cplusplus
 extern "C" {
 #endif
-/* Select the single-channel kernel: 0 = persistent workgroups (default, ddc_persistent.hip),
- * 1 = one workgroup per frame (v1), 3 = one wave per frame at d = 0 (ddc_wave.hip),
- * 4 = two frames in flight per workgroup at d = 0 (r2iq_pipe_kernel), 5 = radix 8 with 512
- * threads per frame at d = 0 (r2iq_r8_kernel), 6 = lane pairs, 512 threads per frame at d = 0
- * (r2iq_pair_kernel), 7 = in-place LDS passes at d = 0 (r2iq_inplace_kernel); 3..7 run the
- * persistent kernel at d > 0.  Used by tools/ab_kernels.py to time variants in one process. */
-int sddc_ddc_internal_set_variant(sddc_ddc_t *h, int variant);
 /* A tuning parameter of the kernels (A/B timing, tools/ab_libs.py --param):
  * SDDC_DDC_PARAM_FS_STATIC_PCT = the d = 0 kernel's share of each workgroup's frames taken
  * statically before it draws from the dynamic queue (0..100, default kFsStaticPct). */
@@ -32,8 +25,10 @@ int sddc_ddc_internal_set_variant(sddc_ddc_t *h, int variant);
 /* SDDC_DDC_PARAM_FS_STEAL_PUBLIC: frames at the end of each workgroup's range open to thieves,
  * claimed by the owner with atomics (0: all but the first two); the rest the owner takes alone. */
 #define SDDC_DDC_PARAM_FS_STEAL_PUBLIC 6
-/* SDDC_DDC_PARAM_FS_ZERO_ROWS = 1 (default): the d = 0 kernel skips the inverse input's whole zero
- * rows of the tune bin (4 rows when tb <= 1024 or tb >= 3072); 0: computes them (A/B). */
+/* SDDC_DDC_PARAM_FS_ZERO_ROWS != 0 (default 1): the d = 0 kernel skips the inverse input's whole
+ * zero rows of the tune bin (ddc_fs.hip fs_zero_rows: 2..8 rows for CF32 output without the NCO,
+ * 4 rows or none for the fused-NCO and CS16 outputs and the queue / stealing schedules; a single
+ * zero row is computed); 0: computes them all (A/B, tests). */
 #define SDDC_DDC_PARAM_FS_ZERO_ROWS 7
 
 int sddc_ddc_internal_set_param(sddc_ddc_t *h, int param, int value);

@@ -10,7 +10,6 @@ if ROOT not in sys.path:
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (gfx950) and the built HIP library")
-    config.addinivalue_line("markers", "variants: exercises the A/B kernel variants (libsddc_ddc_variants.so)")
 
 
 def gpu_available() -> bool:

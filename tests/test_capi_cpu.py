@@ -96,16 +96,18 @@ def test_null_handle_errors(ddc_lib):
     assert ddc_lib.sddc_ddc_kaiser(0, 120.0, 0.4, 0.5, None) > 0
 
 
-def test_variant_kernels_live_outside_the_product_library(ddc_lib):
-    """The measured-slower A/B kernels are built into libsddc_ddc_variants.so, not into the
-    product library (which loads them only when a handle selects a variant)."""
+def test_product_library_is_self_contained(ddc_lib):
+    """The product library holds the product kernels only and loads no other library at run
+    time: no dlopen / dlsym imports (round 5 loaded the measured-slower A/B kernels from a second
+    library on request; they are in git history now), no A/B kernel symbols."""
     import subprocess
     from extio_sddc_amd._lib import LIB_PATH
-    var = os.path.join(os.path.dirname(LIB_PATH), "libsddc_ddc_variants.so")
-    assert os.path.exists(var)
     prod = subprocess.run(["nm", "-C", LIB_PATH], capture_output=True, text=True).stdout
-    vsym = subprocess.run(["nm", "-C", "-D", "--defined-only", var], capture_output=True, text=True).stdout
-    for k in ("r2iq_pipe_kernel", "r2iq_r8_kernel", "r2iq_wave_kernel", "r2iq_frame_kernel"):
+    undef = subprocess.run(["nm", "-D", "--undefined-only", LIB_PATH], capture_output=True, text=True).stdout
+    for k in ("r2iq_pipe_kernel", "r2iq_r8_kernel", "r2iq_wave_kernel", "r2iq_frame_kernel", "sddc_variants_get",
+              "sddc_ddc_internal_set_variant"):
         assert k not in prod, k
-    assert "r2iq_persistent_kernel" in prod
-    assert "sddc_variants_get" in vsym
+    for k in ("r2iq_persistent_kernel", "r2iq_fs_kernel", "r2iq_channels"):
+        assert k in prod, k
+    assert not any(f" {s}" in undef for s in ("dlopen", "dlsym", "dlmopen")), undef
+    assert not os.path.exists(os.path.join(os.path.dirname(LIB_PATH), "libsddc_ddc_variants.so"))

@@ -263,7 +263,8 @@ def test_table_rebuild_seen_by_other_stream(torch_dev, ddc, oracle, H, d, tb0, t
 
 
 # sddc_ddc_internal.h SDDC_DDC_PARAM_*
-P_FS_STATIC_PCT, P_SLOT_WEIGHTS, P_FS_SCHEDULE, P_FS_MINREM, P_FS_PUBLIC, P_FS_ZERO_ROWS = 1, 2, 4, 5, 6, 7
+P_FS_STATIC_PCT, P_SLOT_WEIGHTS, P_FS_FRAMES_PER_WG, P_FS_SCHEDULE, P_FS_MINREM, P_FS_PUBLIC, P_FS_ZERO_ROWS = \
+    1, 2, 3, 4, 5, 6, 7
 
 
 def _set_param(r, param, value):
@@ -278,11 +279,14 @@ def _set_param(r, param, value):
 SCHEDULES = {
     # d = 0 (FS kernel): the static split (default), the queue at static shares 100 / 40 / 0 %,
     # work stealing (every frame open / the last 4 of each range, steal threshold 2 / disabled),
-    # and the zero rows computed instead of skipped
+    # the zero rows computed instead of skipped, and non-persistent grids (16 frames per
+    # workgroup: 1408 workgroups, XCD-mapped ranges) with the static split and with work stealing
+    # (the steal slots indexed by the mapped range, ddc_queue.hpp StealSchedule::self)
     0: [(), ((P_FS_SCHEDULE, 1), (P_FS_STATIC_PCT, 100)), ((P_FS_SCHEDULE, 1), (P_FS_STATIC_PCT, 40)),
         ((P_FS_SCHEDULE, 1), (P_FS_STATIC_PCT, 0)), ((P_FS_SCHEDULE, 2),),
         ((P_FS_SCHEDULE, 2), (P_FS_PUBLIC, 4), (P_FS_MINREM, 2)), ((P_FS_SCHEDULE, 2), (P_FS_MINREM, 0)),
-        ((P_FS_ZERO_ROWS, 0),)],
+        ((P_FS_ZERO_ROWS, 0),), ((P_FS_FRAMES_PER_WG, 16),),
+        ((P_FS_SCHEDULE, 2), (P_FS_FRAMES_PER_WG, 16), (P_FS_MINREM, 2))],
     # persistent kernel: slot-weighted vs equal contiguous split
     1: [(), ((P_SLOT_WEIGHTS, 0),)],
     4: [(), ((P_SLOT_WEIGHTS, 0),)],
@@ -316,45 +320,88 @@ def test_schedules_bit_identical(torch_dev, d):
         np.testing.assert_array_equal(o, outs[0], err_msg=str(settings))
 
 
+def fs_zero_rows(tb):
+    """ddc_fs.hip fs_zero_rows: the whole zero rows of the d = 0 inverse input that the FS kernel
+    skips for tune bin tb (> 0 at the top, < 0 at the bottom; a single zero row is computed)"""
+    top = 16 - (tb + 2048 + 255) // 256
+    bot = (tb - 2048) // 256 if tb > 2048 else 0
+    z = top if top > 0 else -bot if bot > 0 else 0
+    z = max(-8, min(8, z))
+    return 0 if abs(z) == 1 else z
+
+
 # d = 0 tune bins by the inverse input's whole zero rows (the reference's zero fill,
 # impl.hpp:91-96): (tb, rows zero at the top (bins >= tb + 2048), rows zero at the bottom
-# (bins < tb - 2048)); the FS kernel skips 4 of them when there are 4 or more (ZR = +-4)
-ZERO_ROW_BINS = [(2048, 0, 0), (1792, 1, 0), (1028, 3, 0), (1024, 4, 0), (256, 7, 0), (0, 8, 0),
-                 (2304, 0, 1), (3068, 0, 3), (3072, 0, 4), (3840, 0, 7), (4092, 0, 7)]
+# (bins < tb - 2048)).  The FS kernel is instantiated per count (ddc_fs.hip launch_fs_v: 2..8 at
+# the top, 2..7 at the bottom for CF32 output without the NCO; 4 or none for the NCO / CS16
+# outputs), so every count it can select has a tune bin here, most of them two.
+ZERO_ROW_BINS = [(2048, 0, 0), (1792, 1, 0), (1536, 2, 0), (1284, 2, 0), (1028, 3, 0), (1024, 4, 0),
+                 (768, 5, 0), (724, 5, 0), (512, 6, 0), (260, 6, 0), (256, 7, 0), (0, 8, 0),
+                 (2304, 0, 1), (2560, 0, 2), (2812, 0, 2), (3068, 0, 3), (3072, 0, 4), (3328, 0, 5),
+                 (3580, 0, 5), (3584, 0, 6), (3836, 0, 6), (3840, 0, 7), (4092, 0, 7)]
 
 
-@pytest.mark.parametrize("tb,ztop,zbot", ZERO_ROW_BINS)
-def test_fs_zero_rows(torch_dev, oracle, H, tb, ztop, zbot):
-    """The zero-row skip at tune bins giving 0, 1, 3, 4, 7 and 8 zero rows (top and bottom):
-    within 1e-5 of the f64 oracle (4 blocks, strong out-of-band + weak in-band tone and a mix),
-    and equal to the same launch with the zero rows computed (64 blocks, NaN-filled)"""
-    torch = torch_dev
+def _zero_rows_case(torch, oracle, H, tb, lsb=0, rand=0):
+    """4 blocks of each source against the f64 oracle, then 64 blocks with the zero rows skipped
+    against the same launch with them computed (NaN-filled outputs, bit-identical)"""
     from extio_sddc_amd import R2iq, output_samples
     from extio_sddc_amd.synth import make_stream
-    assert (2048 - tb) // 256 == ztop if tb <= 2048 else (tb - 2048) // 256 == zbot
+
+    def launch(r, d_in, nblk):
+        r.setDecimate(0)
+        r.setTuneBin(tb)
+        r.setSideband(bool(lsb))
+        r.updateRand(bool(rand))
+        out = torch.full((output_samples(0, nblk) * 2,), float("nan"), dtype=torch.float32, device="cuda")
+        r.process_device(d_in, nblk, out)
+        torch.cuda.synchronize()
+        return out.cpu().numpy()
+
     for src in ("mix", "oob"):
         x = make_stream(4, src)
         with R2iq(gain=1.0, device=0) as r:
-            r.setDecimate(0)
-            r.setTuneBin(tb)
-            d_in = torch.from_numpy(x).to("cuda")
-            out = torch.full((output_samples(0, 4) * 2,), float("nan"), dtype=torch.float32, device="cuda")
-            r.process_device(d_in, 4, out)
-            torch.cuda.synchronize()
-        y = out.cpu().numpy().view(np.complex64)
-        err = oracle.max_rel_err(y, oracle.r2iq(x, 4, 0, tb, H=H))
+            y = launch(r, torch.from_numpy(x).to("cuda"), 4).view(np.complex64)
+        err = oracle.max_rel_err(y, oracle.r2iq(x, 4, 0, tb, lsb, rand, H=H))
         assert err <= TOL, f"{src}: max-rel-err {err:.3e}"
     nblk = 64
     d_in = device_stream(torch, nblk, 0x5DDC + tb)
     outs = []
     for zr in (1, 0):
         with R2iq(gain=1.0, device=0) as r:
-            r.setDecimate(0)
-            r.setTuneBin(tb)
             _set_param(r, P_FS_ZERO_ROWS, zr)
-            out = torch.full((output_samples(0, nblk) * 2,), float("nan"), dtype=torch.float32, device="cuda")
-            r.process_device(d_in, nblk, out)
-            torch.cuda.synchronize()
-            outs.append(out.cpu().numpy())
+            outs.append(launch(r, d_in, nblk))
     assert np.all(np.isfinite(outs[0]))
     np.testing.assert_array_equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("tb,ztop,zbot", ZERO_ROW_BINS)
+def test_fs_zero_rows(torch_dev, oracle, H, tb, ztop, zbot):
+    """The zero-row skip at tune bins giving 0 to 8 zero rows at the top and 0 to 7 at the bottom
+    (every instance the plain CF32 output can select): within 1e-5 of the f64 oracle (4 blocks,
+    strong out-of-band + weak in-band tone and a mix), and equal to the same launch with the zero
+    rows computed (64 blocks, NaN-filled)"""
+    assert (2048 - tb) // 256 == ztop if tb <= 2048 else (tb - 2048) // 256 == zbot
+    _zero_rows_case(torch_dev, oracle, H, tb)
+
+
+# the RAND and LSB instances at every count they are built for (ddc_fs.hip launch_fs_v: the same
+# counts as the plain output), each count once, both options on; ZR = 4 (tb = 1024) is in the
+# C4-style cases of test_gpu_parity.py too
+ZERO_ROW_BINS_RL = [(1536, 2), (1028, 3), (1024, 4), (768, 5), (512, 6), (256, 7), (0, 8),
+                    (2560, -2), (3068, -3), (3072, -4), (3328, -5), (3584, -6), (3840, -7)]
+
+
+@pytest.mark.parametrize("tb,zr", ZERO_ROW_BINS_RL)
+def test_fs_zero_rows_rand_lsb(torch_dev, oracle, H, tb, zr):
+    """The RAND + LSB kernel instances of every zero-row count: 1e-5 vs the f64 oracle with
+    de-randomisation and sideband inversion on, and skip on = skip off bit for bit"""
+    assert fs_zero_rows(tb) == zr
+    _zero_rows_case(torch_dev, oracle, H, tb, lsb=1, rand=1)
+
+
+def test_fs_zero_row_counts_covered():
+    """CPU-side: the tune-bin lists reach every zero-row count launch_fs_v instantiates"""
+    counts = {fs_zero_rows(tb) for tb, _, _ in ZERO_ROW_BINS}
+    assert counts >= {0, 2, 3, 4, 5, 6, 7, 8, -2, -3, -4, -5, -6, -7}
+    assert {zr for _, zr in ZERO_ROW_BINS_RL} == {2, 3, 4, 5, 6, 7, 8, -2, -3, -4, -5, -6, -7}
+    assert all(fs_zero_rows(tb) != -8 for tb in range(0, 4096, 4))   # ZR = -8 is never selected

@@ -1,13 +1,11 @@
 """Seeded random parity sweep on a real MI355X (pytest -m gpu): 48 configurations drawn from
 d in 0..6, any legal tune bin (multiple of 4, the setFreqOffset grid, fft_mt_r2iq.cpp:104),
 sideband, rand, the synthetic sources and 1..5 blocks, each checked against the f64 oracle.
-At d = 0 the A/B variants of libsddc_ddc_variants.so (the wave kernel, variant 3; two frames in
-flight, variant 4; radix 8, variant 5; lane pairs, variant 6; in-place passes, variant 7) are checked on the same case as well.
 
 Bar: IQ max-rel-err <= 1e-5 (north_star) for every channel whose output reaches -40 dB of
 full scale; a channel below that is "leakage-only": its strict error is held to the float32
-floor (<= 2x the oracle's float32 port of the reference algorithm on the same input; the
-distribution over 24 such draws is in test_gpu_floor.py), and, as the documented secondary, its
+floor (<= 1.2x the oracle's float32 port of the reference algorithm on the same input, the bar of
+the 24 draws of test_gpu_floor.py), and, as the documented secondary, its
 error measured against the -40 dB level (``leak_aware_err``) to 1e-5.
 
 Full scale S = 1024 * max|x|: the peak IQ an in-band tone of the input's peak amplitude gives at
@@ -21,7 +19,6 @@ float32 FFT path, the reference's FFTW included): the three leakage-only draws s
 5.6e-6, 1.5e-6 and 2.0e-6; every other draw is at >= -36 dB and held to the strict bar."""
 from __future__ import annotations
 
-import ctypes
 import json
 import os
 
@@ -34,6 +31,7 @@ pytestmark = pytest.mark.gpu
 
 TOL = 1e-5
 LEAK_DB = -40.0   # below this level (re full scale) a channel is leakage-only
+FLOOR_FACTOR = 1.2   # a leakage-only draw's strict error against the float32 port's (test_gpu_floor.py)
 SOURCES = ["mix", "uniform", "bench", "oob"]
 
 
@@ -69,7 +67,6 @@ def ddc():
     assert torch.cuda.is_available(), "gpu tests need a GPU"
     from extio_sddc_amd import R2iq
     r = R2iq(gain=1.0, device=0)
-    r._L.sddc_ddc_internal_set_variant.argtypes = [ctypes.c_void_p, ctypes.c_int]
     yield r
     r.close()
 
@@ -87,39 +84,36 @@ def H32(oracle):
 @pytest.mark.parametrize("d,tb,lsb,rand,src,nblk,seed", _cases())
 def test_random_config_parity(ddc, oracle, H, H32, d, tb, lsb, rand, src, nblk, seed):
     import torch
-    from extio_sddc_amd import _lib, output_samples
+    from extio_sddc_amd import output_samples
     x = make_stream(nblk, src, seed=seed)
     r = oracle.r2iq(x, nblk, d, tb, lsb, rand, H=H)
     d_in = torch.from_numpy(x).to("cuda")
-    for variant in ([0, 3, 4, 5, 6, 7] if d == 0 else [0]):
-        _lib.check(ddc._L.sddc_ddc_internal_set_variant(ddc._h, variant))
-        try:
-            ddc.setDecimate(d)
-            ddc.setTuneBin(tb)
-            ddc.setSideband(bool(lsb))
-            ddc.updateRand(bool(rand))
-            out = torch.full((output_samples(d, nblk) * 2,), float("nan"), dtype=torch.float32, device="cuda")
-            ddc.process_device(d_in, nblk, out)
-            torch.cuda.synchronize()
-        finally:
-            _lib.check(ddc._L.sddc_ddc_internal_set_variant(ddc._h, 0))
-        y = out.cpu().numpy().view(np.complex64)
-        assert np.all(np.isfinite(y))
-        err, leak = leak_aware_err(y, r, x)
-        if leak:
-            # primary: at the float32 floor, i.e. within 2x of the oracle's float32 port of the
-            # reference algorithm on the same input (test_gpu_floor.py holds the distribution of
-            # the ratio over 24 such draws to a geometric mean <= 1); the -40 dB rule stays as the
-            # documented secondary
-            port = oracle.r2iq(x, nblk, d, tb, lsb, rand, dtype=np.float32, H=H32)
-            strict, port_err = oracle.max_rel_err(y, r), oracle.max_rel_err(port, r)
-            _record({"test": "sweep leakage-only draw", "d": d, "tunebin": tb, "lsb": lsb, "rand": rand,
-                     "source": src, "nblk": nblk, "seed": seed, "variant": variant,
-                     "peak_db_re_full_scale": 20 * np.log10(float(np.max(np.abs(r))) / (1024.0 * float(
-                         np.abs(x.astype(np.float64)).max()))),
-                     "strict_max_rel_err": strict, "port_f32_max_rel_err": port_err, "leakage_aware_err": err})
-            assert strict <= 2.0 * port_err, f"variant {variant}: leakage-only draw {strict:.3e} > 2 x port {port_err:.3e}"
-        assert err <= TOL, f"variant {variant}: {'leakage-aware' if leak else 'max-rel'} err {err:.3e}"
+    ddc.setDecimate(d)
+    ddc.setTuneBin(tb)
+    ddc.setSideband(bool(lsb))
+    ddc.updateRand(bool(rand))
+    out = torch.full((output_samples(d, nblk) * 2,), float("nan"), dtype=torch.float32, device="cuda")
+    ddc.process_device(d_in, nblk, out)
+    torch.cuda.synchronize()
+    y = out.cpu().numpy().view(np.complex64)
+    assert np.all(np.isfinite(y))
+    err, leak = leak_aware_err(y, r, x)
+    if leak:
+        # primary: at the float32 floor, i.e. within FLOOR_FACTOR = 1.2x of the oracle's float32
+        # port of the reference algorithm on the same input, the bar test_gpu_floor.py holds
+        # its 24 leakage draws to (the float32 model of the kernel, tools/fp32_model.py, puts
+        # this sweep's three leakage-only draws at 0.89, 0.92 and 0.75x the port); the -40 dB
+        # rule stays as the documented secondary
+        port = oracle.r2iq(x, nblk, d, tb, lsb, rand, dtype=np.float32, H=H32)
+        strict, port_err = oracle.max_rel_err(y, r), oracle.max_rel_err(port, r)
+        _record({"test": "sweep leakage-only draw", "d": d, "tunebin": tb, "lsb": lsb, "rand": rand,
+                 "source": src, "nblk": nblk, "seed": seed,
+                 "peak_db_re_full_scale": 20 * np.log10(float(np.max(np.abs(r))) / (1024.0 * float(
+                     np.abs(x.astype(np.float64)).max()))),
+                 "strict_max_rel_err": strict, "port_f32_max_rel_err": port_err, "leakage_aware_err": err})
+        assert strict <= FLOOR_FACTOR * port_err, \
+            f"leakage-only draw {strict:.3e} > {FLOOR_FACTOR} x port {port_err:.3e}"
+    assert err <= TOL, f"{'leakage-aware' if leak else 'max-rel'} err {err:.3e}"
 
 
 def _channel_cases(seed=0x5DDC + 1):

@@ -28,7 +28,6 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--tunebin", type=int, default=1024)
     ap.add_argument("--channels", type=int, default=0, help="time process_channels_device with tune bins 4c")
-    ap.add_argument("--variant", type=int, default=0, help="single-channel kernel (sddc_ddc_internal.h)")
     ap.add_argument("--rand", action="store_true", help="RAND de-randomisation on (config C4)")
     ap.add_argument("--lsb", action="store_true", help="sideband inversion on (config C4)")
     ap.add_argument("--input", choices=["rand", "bench", "zeros"], default="rand",
@@ -55,9 +54,6 @@ def main():
             assert L.sddc_ddc_set_rand(h, 1) == 0
         if args.lsb:
             assert L.sddc_ddc_set_sideband(h, 1) == 0
-        if args.variant:
-            L.sddc_ddc_internal_set_variant.argtypes = [ctypes.c_void_p, ctypes.c_int]
-            assert L.sddc_ddc_internal_set_variant(h, args.variant) == 0
         for kv in filter(None, params.split(",")):
             k, v = (int(x) for x in kv.split("="))
             L.sddc_ddc_internal_set_param.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
