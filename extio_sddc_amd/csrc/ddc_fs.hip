@@ -11,8 +11,9 @@
 //                                            -> LDS
 //   I1 table twiddles + DFT-16               -> LDS
 //   I2 twiddles g_t W^{-t r} + DFT-16, quarter turns, overlap-discard IQ stores.
-// Every exchange writes in place of its own reads (padded 17-slot rows, below), so a frame has
-// four barriers and every LDS access is one base plus a per-register immediate.
+// Every exchange writes in place of its own reads (the pair-interleaved row layout fs_slot,
+// below), so a frame has four barriers, every LDS access is one base plus a per-register
+// immediate, and no access has a bank conflict.
 //
 // The fused split.  F2's butterfly on lane l is column c = kFsPerm[l]: it produces Z[c + 256 k],
 // k = 0..15.  The split of bin b needs Z[-b]; for b = c + 256 k that is Z[(256 - c) + 256 (15 - k)],
@@ -127,12 +128,35 @@ __device__ __forceinline__ void emit_frame_q(void *__restrict__ out, int fbase, 
 
 // The queue wave (not wave 0, which also carries the self-mirrored columns' split)
 constexpr int kQWave = 3;
-// The exchanges' LDS layout: element 16 R + j (row R, column j) at 17 R + j + [R >= 128].  F0's
-// row stores and I2's row reads are conflict-free, F2's reads and I0's stores too (with
-// kFsPerm, tools/fs_perm.py); F1's and I1's reads of 272-slot strides have one 2-way bank
-// conflict per 32 lanes, which no lane assignment removes on 17-slot rows (DESIGN.md §4.1,
-// round 5).  tests/test_fs_model.py checks every exchange's delivery and in-place property.
-constexpr int kFsLds = HALF + HALF / 16;
+// fs_slot(t, 0): the F0 / I2 row of thread t
+__device__ __forceinline__ int fs_row_slot(int t) { return 272 * (t >> 4) + (t >= 128) + 34 * ((t & 15) >> 1) + (t & 1); }
+// fs_pair_lane: F1's and I1's thread t takes row u = 2 (t >> 5) + (t & 1) of each 16-row block,
+// column j = (t >> 1) & 15: its base slot fs_slot(u, j) = 34 (t >> 5) + (t & 31) = t + 2 (t >> 5)
+// (the block's 272 r + [r >= 8] is the immediate)
+__device__ __forceinline__ int fs_pair_row(int t) { return 2 * (t >> 5) + (t & 1); }
+__device__ __forceinline__ int fs_pair_col(int t) { return (t >> 1) & 15; }
+__device__ __forceinline__ int fs_pair_slot(int t) { return t + 2 * (t >> 5); }
+// The exchanges' LDS layout (round 6): row R (0..255), column j (0..15) at
+//   fs_slot(R, j) = 272 (R >> 4) + [R >= 128] + 34 ((R & 15) >> 1) + (R & 1) + 2 j:
+// rows 2i and 2i + 1 of a 16-row block interleave (even and odd slots) in a 32-slot run, the runs
+// 34 slots apart.  The access patterns (gfx950 banking, MI355X_MICROARCH.md LDS table: a
+// ds_read_b64 serves 32-lane groups, conflict-free iff the slots differ mod 32; ds_write_b64
+// 16-lane groups, mod 16), each one base plus a per-register immediate:
+//   F0 stores / I2 reads: thread t's row t, base fs_slot(t, 0) + 2 r: slot = (t & 15) + 2 r
+//     mod 16 and 16 ((t >> 4) & 1) + (t & 15) + 2 r mod 32 (272 = 16 mod 32);
+//   F1, I1 (reads and in-place stores): thread t takes the row pair q = t >> 5, row
+//     u = 2 q + (t & 1), column j = (t >> 1) & 15 (fs_pair_lane): slots 34 q + (t & 31) + 272 r
+//     + [r >= 8], 32 consecutive per 32-lane group;
+//   F2 reads / I0 stores: column c = 16 h + cl reads rows 16 h + r, column cl: base
+//     272 h + [h >= 8] + 2 cl, immediate 34 (r >> 1) + (r & 1), conflict-free for kFsPerm
+//     (tools/fs_perm.py; the odd upper-half pad keeps the lane pairs c, 256 - c apart).
+// Round 5's 17-slot rows left one 2-way conflict per 32 lanes on every F1 and I1 read (11 % of the
+// LDS cycles), which no lane assignment removes on contiguous rows.  A skewed layout with the F0
+// rows permuted across lanes (fs_slot 264-slot blocks, rows rotated in each 32-lane run) was
+// conflict-free too but 4 % slower: its input loads and IQ stores were no longer in lane order
+// (DESIGN.md §4.1, round 6).  tests/test_fs_model.py checks every exchange's delivery, the in-place
+// property and the bank keys.
+constexpr int kFsLds = 4352;
 // twiddle bases W^j (j < 256) at j + [j >= 128], W^{4j} kFsTw later: F2 reads them at its column
 // c = kFsPerm[t], whose key c + [c >= 128] the permutation keeps distinct mod 32 over 32 lanes
 // (tools/fs_perm.py), I2 at t; both ds_read_b64 and conflict-free.  (Unpadded, the lane pairs
@@ -232,7 +256,6 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
         asm volatile("" : "+s"(z));
         const int t = tid + z;
         const int c = col_ + z;
-        const int x15 = t & 15;
         const int oblk = blk * 8 * HALF;
         const int kc = k;
         // ---- F0 (R16, NS1): convert + DFT16 from registers ----
@@ -254,24 +277,24 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
         // no barrier: this thread's row is exactly what it read in the previous frame's inverse
         // pass 2 (every exchange writes in place of its own reads)
         {
-            float2 *const row = lds + 17 * t + (t >= 128);
+            float2 *const row = lds + fs_row_slot(t);
 #pragma unroll
-            for (int r = 0; r < 16; r++) row[r] = v[r];
+            for (int r = 0; r < 16; r++) row[2 * r] = v[r];
         }
         ST_SYNC(1);
-        // ---- F1 (R16, NS16): table twiddles W_256^{(t%16) r} ----
+        // ---- F1 (R16, NS16): table twiddles W_256^{j r} ----
+        // rows 16 r + u, column j of the thread's pair lane (u, j) (fs_pair_lane)
         {
             float2 a[16];
-            const float2 *const col = lds + t + (t >> 4);
+            const float2 *const col = lds + fs_pair_slot(t);
 #pragma unroll
             for (int r = 0; r < 16; r++) XRD(a[r], col[272 * r + (r >= 8)]);
-            table_twiddle<-1, true>(a, twl, 16, x15);
+            table_twiddle<-1, true>(a, twl, 16, fs_pair_col(t));
             dft16<-1>(a, v);
         }
         {
-            // in place of the reads (no barrier): element 256 (t >> 4) + 16 r + x15 at
-            // t + (t >> 4) + 272 r + [r >= 8], ds_write_b64 groups of 16 lanes conflict-free
-            float2 *const col = lds + t + (t >> 4);
+            // in place of the reads (no barrier)
+            float2 *const col = lds + fs_pair_slot(t);
 #pragma unroll
             for (int r = 0; r < 16; r++) col[272 * r + (r >= 8)] = v[r];
         }
@@ -291,12 +314,12 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
         asm volatile("" ::: "memory");
         {
             float2 a[16];
-            // element c + 256 g (F1 thread 16 g + (c & 15), its output c >> 4) at
-            // 272 (c >> 4) + (c & 15) + [c >= 128] + 17 g: base + immediate; banks
-            // (c + [c >= 128]) mod 32, conflict-free with kFsPerm (tools/fs_perm.py)
-            const float2 *const cb = lds + 272 * (c >> 4) + (c & 15) + (c >= 128);
+            // F1 output c >> 4 of its pair lanes (r, c & 15): rows 16 (c >> 4) + r, column c & 15
+            // at 272 (c >> 4) + [c >= 128] + 2 (c & 15) + 34 (r >> 1) + (r & 1): base + immediate,
+            // conflict-free with kFsPerm (tools/fs_perm.py)
+            const float2 *const cb = lds + 272 * (c >> 4) + (c >= 128) + 2 * (c & 15);
 #pragma unroll
-            for (int r = 0; r < 16; r++) XRD(a[r], cb[17 * r]);
+            for (int r = 0; r < 16; r++) XRD(a[r], cb[34 * (r >> 1) + (r & 1)]);
             const int cw = c + (c >= 128);
             const float2 fw1 = wtab[cw], fw4 = wtab[kFsTw + cw];   // W^c, W^{4c}
             twiddle_rec16<-1>(a, fw1, fw4);
@@ -356,13 +379,12 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
             dft16z<+1, ZR>(a, u);
         }
         {
-            // in place of this thread's F2 reads (no barrier): output r at 272 (c >> 4) + (c & 15)
-            // + [c >= 128] + 17 r; banks (c + [c >= 128]) mod 16 per 16 lanes, conflict-free
+            // in place of this thread's F2 reads (no barrier): output r at row 16 (c >> 4) + r
             int c1 = c;
             asm volatile("" : "+v"(c1));
-            float2 *const cb = lds + 272 * (c1 >> 4) + (c1 & 15) + (c1 >= 128);
+            float2 *const cb = lds + 272 * (c1 >> 4) + (c1 >= 128) + 2 * (c1 & 15);
 #pragma unroll
-            for (int r = 0; r < 16; r++) cb[17 * r] = u[r];
+            for (int r = 0; r < 16; r++) cb[34 * (r >> 1) + (r & 1)] = u[r];
         }
         // the next frame (phase B: the schedule's, from the ticket read at this frame's top;
         // ddc_queue.hpp)
@@ -379,13 +401,12 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
         const unsigned t8 = 8u * (unsigned)t;
         const float2 g0 = buf_load8(rfs, t8, 0), g1 = buf_load8(rfs, t8, 8u * NT), g4 = buf_load8(rfs, t8, 16u * NT);
         int fn;
-        // ---- I1 (R16, NS16): table twiddles W_256^{-(t%16) r} ----
+        // ---- I1 (R16, NS16): table twiddles W_256^{-s r} ----
         {
             float2 a[16];
-            // element t + 256 r was stored by I0 column (t >> 4) + 16 r (its output t & 15) at
-            // 272 r + [r >= 8] + (t >> 4) + 17 (t & 15): base + immediate, one 2-way bank conflict
-            // per 32 lanes (as F1's loads)
-            const float2 *const ib = lds + (t >> 4) + 17 * x15;
+            // I0 output s of columns 16 r + cl, for the pair lane (s, cl) = (u, j) of this
+            // thread (fs_pair_lane): rows 16 r + s, column cl, the slots F1 used
+            const float2 *const ib = lds + fs_pair_slot(t);
 #pragma unroll
             for (int r = 0; r < 16; r++) XRD(a[r], ib[272 * r + (r >= 8)]);
             // the next frame's number is read behind the data reads (its LDS round trip under
@@ -403,15 +424,15 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
             // for I2's lane factors included the atomic); read at the next frame's top
             if constexpr (PB)
                 if (qw) fsch.take();
-            table_twiddle<+1, true>(a, twl, 16, x15);
+            table_twiddle<+1, true>(a, twl, 16, fs_pair_row(t));
             dft16<+1>(a, u);
         }
         {
             // in place of this thread's I1 reads (no barrier), recomputed from an opaque copy of
-            // t (else kept live through the pass): element 256 (t >> 4) + 16 r + (t & 15)
+            // t (else kept live through the pass): output g at row 16 g + s, column cl
             int t1 = t;
             asm volatile("" : "+v"(t1));
-            float2 *const ib = lds + (t1 >> 4) + 17 * (t1 & 15);
+            float2 *const ib = lds + fs_pair_slot(t1);
 #pragma unroll
             for (int r = 0; r < 16; r++) ib[272 * r + (r >= 8)] = u[r];
         }
@@ -419,11 +440,11 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
         // ---- I2 (R16, NS256): twiddles g_t W^{-t r}, quarter turns, overlap-discard ----
         {
             float2 a[16];
-            // element t + 256 r (I1 thread 16 r + (t & 15), its output t >> 4) at 17 t + r: the
-            // next frame's F0 row of this thread, conflict-free
-            const float2 *const rb = lds + 17 * t + (t >= 128);
+            // row t (I1 outputs t >> 4 of its pair lanes (t & 15, r)): the next frame's F0 row of
+            // this thread
+            const float2 *const rb = lds + fs_row_slot(t);
 #pragma unroll
-            for (int r = 0; r < 16; r++) XRD(a[r], rb[r]);
+            for (int r = 0; r < 16; r++) XRD(a[r], rb[2 * r]);
             const int tw = t + (t >= 128);
             const float2 rw1 = wtab[tw], rw4 = wtab[kFsTw + tw];   // W^t, W^{4t}
             twiddle_g16<+1>(a, g0, g1, g4, rw1, rw4);
@@ -522,8 +543,9 @@ hipError_t launch_fs_s(const KernelTables &t, const int16_t *d_in, int nblk, voi
 // zero rows of the inverse input for tune bin tb (ZR of r2iq_fs_kernel): the band is
 // [tb - 2048, tb + 2048) clipped to [0, 4096) (the reference's zero fill, impl.hpp:91-96), so rows
 // k >= ceil((tb + 2048) / 256) are zero (tb < 2048, ZR > 0) or rows k < floor((tb - 2048) / 256)
-// (tb > 2048, ZR < 0), at most 8 (dft16z); a single zero row runs unskipped (with it the
-// compiler's schedule of the (P, Q) prefetch spills 5-6 VGPRs)
+// (tb > 2048, ZR < 0), at most 8 (dft16z; 8 only at tb = 0: tb <= 4092 leaves at most 7 at the
+// bottom); a single zero row runs unskipped (with it the compiler's schedule of the (P, Q) prefetch
+// spills 5-6 VGPRs)
 int fs_zero_rows(int tunebin)
 {
     const int top = 16 - (tunebin + 2048 + 255) / 256, bot = tunebin > 2048 ? (tunebin - 2048) / 256 : 0;
@@ -548,8 +570,8 @@ hipError_t launch_fs_z(const KernelTables &t, const int16_t *d_in, int nblk, voi
 }
 
 // the schedule: every output configuration runs the static schedule (the default); work stealing
-// and the queue (A/B, tests) are built for the plain configuration only.  fs.zr: -1 picks the
-// tune bin's zero rows, 0 forces none (A/B)
+// and the queue (A/B, tests) are built for the plain configuration only.  fs.zr != 0 (default):
+// skip the tune bin's zero rows (fs_zero_rows), 0: compute them (A/B, tests)
 template <bool RAND, bool LSB, bool NCO, bool CS16>
 hipError_t launch_fs_v(const KernelTables &t, const int16_t *d_in, int nblk, void *d_out, const float4 *pqf,
                        const float2 *fsl, int tunebin, const OutArgs &oa, const NcoArgs &nco, unsigned *wq,
@@ -566,7 +588,7 @@ hipError_t launch_fs_v(const KernelTables &t, const int16_t *d_in, int nblk, voi
     SDDC_FS_ZR(4) SDDC_FS_ZR(-4)
     if constexpr (FINE) {
         SDDC_FS_ZR(8) SDDC_FS_ZR(7) SDDC_FS_ZR(6) SDDC_FS_ZR(5) SDDC_FS_ZR(3) SDDC_FS_ZR(2)
-        SDDC_FS_ZR(-2) SDDC_FS_ZR(-3) SDDC_FS_ZR(-5) SDDC_FS_ZR(-6) SDDC_FS_ZR(-7) SDDC_FS_ZR(-8)
+        SDDC_FS_ZR(-2) SDDC_FS_ZR(-3) SDDC_FS_ZR(-5) SDDC_FS_ZR(-6) SDDC_FS_ZR(-7)
     }
 #undef SDDC_FS_ZR
     return launch_fs_z<0, RAND, LSB, NCO, CS16>(t, d_in, nblk, d_out, pqf, fsl, tunebin, oa, nco, wq, fs, device, s);

@@ -1,4 +1,4 @@
-"""The d = 0 fused-split kernel's algorithm (ddc_persistent.hip, r2iq_fs_kernel), modelled step
+"""The d = 0 fused-split kernel's algorithm (ddc_fs.hip, r2iq_fs_kernel), modelled step
 by step in numpy (tools/fs_model.py), against the f64 oracle: the lane-paired split (mirror
 from lane ^ 1, register 15 - k), the inverse on absolute bins and the tune shift as the output
 modulation (lane factor g_t + quarter turns).  Also checks the committed lane permutation."""
@@ -20,31 +20,38 @@ from extio_sddc_amd.synth import make_stream  # noqa: E402
 def test_perm_header_is_a_lane_paired_permutation():
     cols = P.read_header()
     assert P.valid(cols)
-    # the in-place layout's I0 stores, F2 loads and F2 twiddle-base loads (W^c at c + [c >= 128]):
-    # conflict-free (keys (c + [c >= 128]) mod 16, 32, 32)
-    assert P.conflicts(cols) == P.BEST["inplace"] == (0, 0, 0)
+    # the il272 layout's I0 stores, F2 loads and F2 twiddle-base loads (W^c at c + [c >= 128]):
+    # conflict-free
+    assert P.conflicts(cols) == P.BEST[P.LAYOUT] == (0, 0, 0)
     # the unpadded twiddle table (key c mod 32) would not be: pairs c, 256 - c = 0 mod 16 collide
     c = np.asarray(cols)
     assert _conflicts(c, 32) > 0 and _conflicts(c + (c >= 128), 32) == 0
 
 
-# The in-place LDS layout of the FS kernel (round 5): every exchange's writer stores into exactly
-# the slots it read in the previous exchange, so only the four read-after-write barriers remain.
-# (thread, register) -> (element, slot) of each store and load, as in ddc_fs.hip.
+def _slot(R, j):
+    return 272 * (R >> 4) + (R >= 128) + 34 * ((R & 15) >> 1) + (R & 1) + 2 * j   # ddc_fs.hip fs_slot
+
+
+# The in-place LDS layout of the FS kernel (round 6, il272): every exchange's writer stores into
+# exactly the slots its threads read in the previous exchange, so only the four read-after-write
+# barriers remain.  (thread, register) -> (element, slot) of each store and load, as in ddc_fs.hip.
 def _layout(perm):
     t = np.arange(256)[:, None]
     r = np.arange(16)[None, :]
     c = np.asarray(perm)[:, None]
-    hi = (r >= 8).astype(int)                     # the padding map's + [e >= 2048]
-    cb = 272 * (c >> 4) + (c & 15) + (c >= 128)
-    ib = (t >> 4) + 17 * (t & 15)
-    fb = 17 * t + (t >= 128)
+    u = 2 * (t >> 5) + (t & 1)                                        # F1 / I1 pair lane: row u,
+    j = (t >> 1) & 15                                                 # column j (fs_pair_lane)
+    assert sorted((16 * u + j).ravel().tolist()) == list(range(256))
+    fb = _slot(t, r)                                                  # F0 stores, I2 loads
+    bb = _slot(16 * r + u, j)                                         # F1 / I1 loads and stores
+    cb = _slot(16 * (c >> 4) + r, c & 15)                             # F2 loads, I0 stores
     return [
-        # (name, store element, store slot, load element, load slot)
-        ("F0->F1", 16 * t + r, fb + r, t + 256 * r, t + (t >> 4) + 272 * r + hi),
-        ("F1->F2", 256 * (t >> 4) + 16 * r + (t & 15), t + (t >> 4) + 272 * r + hi, c + 256 * r, cb + 17 * r),
-        ("I0->I1", 16 * c + r, cb + 17 * r, t + 256 * r, ib + 272 * r + hi),
-        ("I1->I2", 256 * (t >> 4) + 16 * r + (t & 15), ib + 272 * r + hi, t + 256 * r, fb + r),
+        # (name, store element, store slot, load element, load slot): element 16 R + j of the
+        # exchange's row R, column j, numbered by the writer
+        ("F0->F1", 16 * t + r, fb, 16 * (16 * r + u) + j, bb),
+        ("F1->F2", 256 * u + 16 * r + j, bb, c + 256 * r, cb),
+        ("I0->I1", 16 * c + r, cb, 256 * r + 16 * j + u, bb),
+        ("I1->I2", 256 * j + 16 * r + u, bb, t + 256 * r, fb),
     ]
 
 
@@ -81,16 +88,13 @@ def _conflicts(slots, group):
 
 
 def test_inplace_layout_bank_conflicts():
-    # per instruction (one register r), summed over the 4 waves: every store and the F2 / I2 loads
-    # conflict-free; the F1 and I1 loads one 2-way per 32 lanes (the 17-slot rows: t + (t >> 4)
-    # wraps once per 32 lanes), as the round-4 layout's F1 loads
-    lay = _layout(P.read_header())
-    want = {("F0->F1", "st"): 0, ("F0->F1", "ld"): 8, ("F1->F2", "st"): 0, ("F1->F2", "ld"): 0,
-            ("I0->I1", "st"): 0, ("I0->I1", "ld"): 8, ("I1->I2", "st"): 0, ("I1->I2", "ld"): 0}
-    for name, _, ss, _, ls in lay:
+    # per instruction (one register r), summed over the 4 waves: every store and every load
+    # conflict-free (round 5's 17-slot rows left one 2-way conflict per 32 lanes on the F1 and I1
+    # loads: 8 extra cycles per instruction and workgroup)
+    for name, _, ss, _, ls in _layout(P.read_header()):
         for r in range(16):
-            assert _conflicts(ss[:, r], 16) == want[(name, "st")], (name, "st", r)
-            assert _conflicts(ls[:, r], 32) == want[(name, "ld")], (name, "ld", r)
+            assert _conflicts(ss[:, r], 16) == 0, (name, "st", r)
+            assert _conflicts(ls[:, r], 32) == 0, (name, "ld", r)
 
 
 @pytest.mark.parametrize("tb", [0, 4, 284, 1024, 1228, 2048, 3888, 4092])

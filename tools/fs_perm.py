@@ -5,7 +5,8 @@ Lanes 2p, 2p + 1 hold forward-pass-2 columns c, 256 - c (lanes 0, 1: the self-mi
 so the split's mirror bins are one DPP quad_perm [1,0,3,2] away.  Which pair goes to which lane
 pair sets the LDS bank pattern of three accesses (MI355X_MICROARCH.md, LDS: a ds_read_b64 serves
 lane groups of 32 over 64 banks, so slot s = 8-byte index is conflict-free iff s mod 32 is distinct
-over the group; ds_write_b64 / ds_write2_b64 serve groups of 16 over 32 banks: s mod 16 distinct):
+over the group; ds_write_b64 serves 4 groups of 16 contiguous lanes over 32 banks: s mod 16
+distinct):
   * forward pass 2 reads its column's 16 elements, one ds_read_b64 per register (groups of 32);
   * inverse pass 0 stores its 16 outputs in place of those reads (groups of 16);
   * forward pass 2 reads its twiddle bases W^c, W^{4c} (ds_read_b64, groups of 32).
@@ -25,23 +26,38 @@ from collections import Counter
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HDR = os.path.join(ROOT, "extio_sddc_amd", "csrc", "ddc_fs_perm.h")
 
-LAYOUT = "inplace"   # the product's layout (round 5)
+LAYOUT = "il272"   # the product's layout (round 6)
 # the fewest extra cycles (I0 stores, F2 reads, twiddle-base reads) per instruction and workgroup
-BEST = {"inplace": (0, 0, 0)}
+BEST = {"inplace": (0, 0, 0), "il272": (0, 0, 0)}
 WEIGHTS = (16, 16, 2)   # instructions per frame of each access
+
+
+def fs_slot(R: int, j: int) -> int:
+    """ddc_fs.hip fs_slot (round 6): the LDS slot of row R (0..255), column j (0..15): rows 2i and
+    2i + 1 of each 16-row block interleaved in a 32-slot run, runs 34 slots apart, blocks 272
+    apart, the upper half one slot further"""
+    return 272 * (R >> 4) + (R >= 128) + 34 * ((R & 15) >> 1) + (R & 1) + 2 * j
+
+
+def pair_lane(t: int):
+    """ddc_fs.hip fs_pair_row / fs_pair_col: the (row u, column j) of F1's and I1's thread t"""
+    return 2 * (t >> 5) + (t & 1), (t >> 1) & 15
 
 
 def keys(c: int):
     """(inverse pass-0 store key mod 16, forward pass-2 read key mod 32, twiddle-base read key
-    mod 32) of column c"""
-    # in-place exchanges (round 5): F2 reads element c + 256 g at 272 (c >> 4) + (c & 15)
-    # + [c >= 128] + 17 g, and I0 stores its output r at the same slot + 17 r: keys c + [c >= 128].
-    # The odd extra pad of the upper half keeps the lane pairs c, 256 - c apart (c = 1 - c mod 2^k
-    # has no solution), so both can be conflict-free.  The twiddle bases W^j sit at j + [j >= 128]
-    # (ddc_fs.hip kFsTw), the same key, which the unpadded table (c mod 32: the pairs c = 0 mod 16
-    # share it) could not give.
-    k = c + (c >= 128)
-    return k % 16, k % 32, k % 32
+    mod 32) of column c; the twiddle bases W^j sit at j + [j >= 128] (ddc_fs.hip kFsTw)"""
+    if LAYOUT == "inplace":
+        # round 5: F2 reads element c + 256 g at 272 (c >> 4) + (c & 15) + [c >= 128] + 17 g, I0
+        # stores at the same slots
+        k = c + (c >= 128)
+    else:
+        # il272 (round 6): F2 column c = 16 h + cl reads rows 16 h + g, column cl, i.e. slot
+        # fs_slot(16 h, cl) + 34 (g >> 1) + (g & 1); the odd pad of the upper half keeps the lane
+        # pairs c, 256 - c apart, as in round 5
+        k = fs_slot(16 * (c >> 4), c & 15)
+    kt = c + (c >= 128)
+    return k % 16, k % 32, kt % 32
 
 
 def conflicts(cols):
@@ -134,9 +150,11 @@ __constant__ int kFsPerm[256] = {{
 """)
 
 
-def read_header():
+def read_header(name="kFsPerm"):
+    """a table of the committed header (kFsPerm: the lane -> column permutation)"""
     txt = open(HDR).read()
-    body = txt[txt.index("{") + 1:txt.rindex("}")]
+    i = txt.index("{", txt.index(name + "["))
+    body = txt[i + 1:txt.index("}", i)]
     return [int(x) for x in body.replace("\n", " ").split(",") if x.strip()]
 
 
