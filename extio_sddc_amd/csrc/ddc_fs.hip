@@ -56,48 +56,46 @@ __device__ __forceinline__ float dpp_partner(float v)
     return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, true));
 }
 
-// f += conj(zp) q for the bin pair (k, 15 - k), zp = the partner lane's registers: the DPP
-// operand feeds the FMA directly.  s_nop 1: a DPP read of a VGPR needs two wait states after
-// the VALU write of it (the compiler cannot see into the asm).
-__device__ __forceinline__ void split_dpp2(float2 &fa, float2 &fb, float2 za, float2 zb, float4 qa, float4 qb)
+// The split x filter of bin b from the table entry (P, r), r = Q / (i P) real (below):
+//   F = Z_b P + conj(Z_-b) Q = P (Z_b + i r conj(Z_-b)),   Z_b + i r conj(Z_-b) = (Z.x + r Zm.y, Z.y + r Zm.x)
+// with Z_-b the partner lane's register 15 - k: the DPP operand of two FMAs (v_fmac_f32_dpp), then
+// the product with P.  s_nop 1: a DPP read of a VGPR needs two wait states after the VALU write
+// of it (the compiler cannot see into the asm).
+// Both bins of the pair (k, 15 - k): vb (a copy of zb, the register 15 - k) takes its partner term
+// first, while za (register k, updated in place) is still unmodified in every lane; za's own
+// partner term then reads the untouched zb.
+__device__ __forceinline__ void split_v2(float2 &za, float2 &vb, float2 zb, float ra, float rb)
 {
     asm("s_nop 1\n\t"
-        "v_fmac_f32_dpp %0, %4, %8 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %0, %5, %9 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %1, %4, %9 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %1, -%5, %8 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %2, %6, %10 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %2, %7, %11 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %3, %6, %11 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %3, -%7, %10 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf"
-        : "+v"(fa.x), "+v"(fa.y), "+v"(fb.x), "+v"(fb.y)
-        : "v"(za.x), "v"(za.y), "v"(zb.x), "v"(zb.y), "v"(qa.z), "v"(qa.w), "v"(qb.z), "v"(qb.w));
+        "v_fmac_f32_dpp %2, %1, %7 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %3, %0, %7 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %0, %5, %6 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %1, %4, %6 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf"
+        : "+v"(za.x), "+v"(za.y), "+&v"(vb.x), "+&v"(vb.y)
+        : "v"(zb.x), "v"(zb.y), "v"(ra), "v"(rb));
 }
 
-// one half of split_dpp2: f += conj(z of the partner lane) q
-__device__ __forceinline__ void split_dpp1(float2 &f, float2 z, float4 q)
+// one bin: z += i r conj(z of the partner lane), in place (the partner's register is not written)
+__device__ __forceinline__ void split_v1(float2 &z, float2 zp, float r)
 {
     asm("s_nop 1\n\t"
-        "v_fmac_f32_dpp %0, %2, %4 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %0, %3, %5 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %1, %2, %5 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
-        "v_fmac_f32_dpp %1, -%3, %4 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf"
-        : "+v"(f.x), "+v"(f.y)
-        : "v"(z.x), "v"(z.y), "v"(q.z), "v"(q.w));
+        "v_fmac_f32_dpp %0, %3, %4 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+        "v_fmac_f32_dpp %1, %2, %4 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf"
+        : "+v"(z.x), "+v"(z.y)
+        : "v"(zp.x), "v"(zp.y), "v"(r));
 }
 
-// Zk P (own registers)
-__device__ __forceinline__ float2 zk_p(float2 zk, float4 c)
+// F = P V for the table entry q = (P.x, P.y, r)
+__device__ __forceinline__ float2 p_mul(float2 v, float3 q)
 {
-    return make_float2(fmaf(zk.x, c.x, -zk.y * c.y), fmaf(zk.x, c.y, zk.y * c.x));
+    return make_float2(fmaf(v.x, q.x, -v.y * q.y), fmaf(v.x, q.y, v.y * q.x));
 }
-__device__ __forceinline__ float2 zc_q(float2 f, float2 zc, float4 c)
+
+__device__ __forceinline__ float3 buf_load12(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff)
 {
-    f.x = fmaf(zc.x, c.z, f.x);
-    f.x = fmaf(zc.y, c.w, f.x);
-    f.y = fmaf(zc.x, c.w, f.y);
-    f.y = fmaf(-zc.y, c.z, f.y);
-    return f;
+    typedef unsigned u32x3 __attribute__((ext_vector_type(3)));
+    const u32x3 v = __builtin_amdgcn_raw_buffer_load_b96(r, voff, soff, 0);
+    return make_float3(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z));
 }
 
 // v (-i)^s, then the sideband flip (imag sign) when LSB: s and LSB are constants after unrolling,
@@ -302,15 +300,15 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
         if constexpr (PB && SCHED == kSchedSteal)
             if (qw) fsch.peek();
         // ---- F2 (R16, NS256) on column c: Z[c + 256 k] in v[k] ----
-        // The split's (P, Q) loads (bin pairs p, 15 - p) run a pair ahead of their use, the first
-        // issued before F2 so that its reads and arithmetic cover the L2 latency (an empty asm
-        // with a memory clobber pins each group; the compiler's own schedule waits for every pair
-        // right after issuing it).  Two pairs ahead of F2 spill at 128 VGPRs.
+        // The split's (P, r) loads (bin pairs p, 15 - p; 12 bytes per bin) run a pair ahead of
+        // their use, the first issued before F2 so that its reads and arithmetic cover the L2
+        // latency (an empty asm with a memory clobber pins each group; the compiler's own schedule
+        // waits for every pair right after issuing it).  Two pairs ahead of F2 spill at 128 VGPRs.
         const __amdgpu_buffer_rsrc_t rpq = buf_rsrc(pqf + z);
-        const unsigned t16 = 16u * (unsigned)t;
-        float4 qa[8], qb[8];
-        if constexpr (!zrow<ZR>(0)) qa[0] = buf_load16(rpq, t16, 0);
-        if constexpr (!zrow<ZR>(15)) qb[0] = buf_load16(rpq, t16, 16u * NT * 15);
+        const unsigned t12 = 12u * (unsigned)t;
+        float3 qa[8], qb[8];
+        if constexpr (!zrow<ZR>(0)) qa[0] = buf_load12(rpq, t12, 0);
+        if constexpr (!zrow<ZR>(15)) qb[0] = buf_load12(rpq, t12, 12u * NT * 15);
         asm volatile("" ::: "memory");
         {
             float2 a[16];
@@ -329,52 +327,68 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
         float2 u[16];
         {
             float2 a[16];
-            if (!w0) {
-#pragma unroll
-                for (int p = 0; p < 8; p++) {
-                    if (p + 1 < 8) {
-                        if (!zrow<ZR>(p + 1)) qa[p + 1] = buf_load16(rpq, t16, 16u * NT * (p + 1));
-                        if (!zrow<ZR>(14 - p)) qb[p + 1] = buf_load16(rpq, t16, 16u * NT * (14 - p));
-                        asm volatile("" ::: "memory");
-                    }
-                    if (zrow<ZR>(15 - p)) {   // row 15 - p zero: row p's half alone
-                        float2 fa = zk_p(v[p], qa[p]);
-                        split_dpp1(fa, v[15 - p], qa[p]);
-                        a[p] = fa;
-                    } else if (zrow<ZR>(p)) {
-                        float2 fb = zk_p(v[15 - p], qb[p]);
-                        split_dpp1(fb, v[p], qb[p]);
-                        a[15 - p] = fb;
-                    } else {
-                        float2 fa = zk_p(v[p], qa[p]), fb = zk_p(v[15 - p], qb[p]);
-                        split_dpp2(fa, fb, v[15 - p], v[p], qa[p], qb[p]);
-                        a[p] = fa;
-                        a[15 - p] = fb;
-                    }
-                }
-            } else {
+            auto split_w0 = [&]() __attribute__((always_inline)) {
                 // wave 0: lanes 0 (column 0: mirror of register k is its own (16 - k) mod 16) and
-                // 1 (column 128: its own 15 - k) are self-mirrored
+                // 1 (column 128: its own 15 - k) are self-mirrored.  Bin 2048 (lane 0, register 8)
+                // has P = 0 (r infinite): its table entry holds Q, and F = Q conj(Z) there.
                 const int lane = t & 63;
 #pragma unroll
                 for (int p = 0; p < 8; p++) {
                     if (p + 1 < 8) {
-                        if (!zrow<ZR>(p + 1)) qa[p + 1] = buf_load16(rpq, t16, 16u * NT * (p + 1));
-                        if (!zrow<ZR>(14 - p)) qb[p + 1] = buf_load16(rpq, t16, 16u * NT * (14 - p));
+                        if (!zrow<ZR>(p + 1)) qa[p + 1] = buf_load12(rpq, t12, 12u * NT * (p + 1));
+                        if (!zrow<ZR>(14 - p)) qb[p + 1] = buf_load12(rpq, t12, 12u * NT * (14 - p));
                         asm volatile("" ::: "memory");
                     }
 #pragma unroll
                     for (int h = 0; h < 2; h++) {
                         const int kk = h ? 15 - p : p;
                         if (zrow<ZR>(kk)) continue;
-                        const float4 q = h ? qb[p] : qa[p];
+                        const float3 q = h ? qb[p] : qa[p];
                         const float2 vm = v[15 - kk], v0m = v[(16 - kk) & 15];
                         float2 zc = make_float2(dpp_partner(vm.x), dpp_partner(vm.y));
                         zc = lane == 1 ? vm : zc;
                         zc = lane == 0 ? v0m : zc;
-                        a[kk] = zc_q(zk_p(v[kk], q), zc, q);
+                        float2 vv = make_float2(fmaf(q.z, zc.y, v[kk].x), fmaf(q.z, zc.x, v[kk].y));
+                        if (kk == 8) vv = lane == 0 ? make_float2(v[8].x, -v[8].y) : vv;
+                        a[kk] = p_mul(vv, q);
                     }
                 }
+            };
+            auto split_generic = [&]() __attribute__((always_inline)) {
+#pragma unroll
+                for (int p = 0; p < 8; p++) {
+                    if (p + 1 < 8) {
+                        if (!zrow<ZR>(p + 1)) qa[p + 1] = buf_load12(rpq, t12, 12u * NT * (p + 1));
+                        if (!zrow<ZR>(14 - p)) qb[p + 1] = buf_load12(rpq, t12, 12u * NT * (14 - p));
+                        asm volatile("" ::: "memory");
+                    }
+                    if (zrow<ZR>(15 - p)) {   // row 15 - p zero: row p's bin alone (v[15 - p] unwritten)
+                        split_v1(v[p], v[15 - p], qa[p].z);
+                        a[p] = p_mul(v[p], qa[p]);
+                    } else if (zrow<ZR>(p)) {
+                        split_v1(v[15 - p], v[p], qb[p].z);
+                        a[15 - p] = p_mul(v[15 - p], qb[p]);
+                    } else {
+                        float2 vb = v[15 - p];
+                        split_v2(v[p], vb, v[15 - p], qa[p].z, qb[p].z);
+                        a[p] = p_mul(v[p], qa[p]);
+                        a[15 - p] = p_mul(vb, qb[p]);
+                    }
+                }
+            };
+            // wave 0's path first, then the generic one, as two ifs on conditions the compiler
+            // cannot relate (an opaque wave index): as an if / else the compiler laid the generic
+            // path out first, so the Z registers it updates in place stayed live for wave 0's path
+            // and every update went through a copy (16 v_mov per wave-frame).  Without zero rows
+            // the two-if form spills 2-4 VGPRs, so ZR = 0 keeps the if / else.
+            if constexpr (ZR != 0) {
+                int wv = __builtin_amdgcn_readfirstlane(t >> 6);
+                asm volatile("" : "+s"(wv));
+                if (w0) split_w0();
+                if (wv != 0) split_generic();
+            } else {
+                if (w0) split_w0();
+                else split_generic();
             }
             dft16z<+1, ZR>(a, u);
         }
@@ -476,10 +490,16 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
         if (tid == QLANE) fs_queue_done(wq, (unsigned)gridDim.x);
 }
 
-// FS tables of one tunebin: pqf[l + 256 k] = (P, Q) of bin b = kFsPerm[l] + 256 k (inverse input
-// m = (b - tb) mod 4096, zero unless b is in the reference's band: tb <= b < tb + 2048, b < 4096,
-// or tb - 2048 <= b < tb); fsl = [g_t | g_t W^{-t} | g_t W^{-4t}], g_t = e^{-2 pi i tb t / 4096},
-// looked up exactly in the 4096-point table.
+// FS tables of one tunebin: pqf[l + 256 k] = (P, r), 12 bytes, of bin b = kFsPerm[l] + 256 k
+// (inverse input m = (b - tb) mod 4096; P and Q = i r P zero unless b is in the reference's band:
+// tb <= b < tb + 2048, b < 4096, or tb - 2048 <= b < tb).  With P = H (1 - i W), Q = H (1 + i W)
+// (H = H_0[m] / 2, W = e^{-2 pi i b / 8192}), r = Q / (i P) = (1 + i W) / (i (1 - i W))
+// = cot(pi/4 - pi b / 8192) is real and does not depend on H or the tune bin; it is infinite only
+// at b = 2048 (column 0, register 8), whose entry holds (Q, 0) instead (the kernel's wave-0 path).
+// Versus the (P, Q) float4 of round 5: 12 bytes per bin instead of 16 (the table is read from L2
+// every frame) and 6 or 7 VALU per bin instead of 8.  tools/fs_model.py (split "pr") models it.
+// fsl = [g_t | g_t W^{-t} | g_t W^{-4t}], g_t = e^{-2 pi i tb t / 4096}, looked up exactly in the
+// 4096-point table.
 __global__ void build_fs_tables_kernel(const float2 *__restrict__ hsel0, const float2 *__restrict__ post8192,
                                        const float2 *__restrict__ tw4096, int tunebin, float4 *__restrict__ pqf,
                                        float2 *__restrict__ fsl)
@@ -489,18 +509,26 @@ __global__ void build_fs_tables_kernel(const float2 *__restrict__ hsel0, const f
     const int l = i & (NT - 1), kk = i >> 8;
     const int b = kFsPerm[l] + NT * kk;
     const bool band = (b >= tunebin && b - tunebin < HALF / 2) || (b < tunebin && tunebin - b <= HALF / 2);
-    float4 c = make_float4(0.f, 0.f, 0.f, 0.f);
+    float3 c = make_float3(0.f, 0.f, 0.f);
     if (band) {
         const int m = (b - tunebin) & (HALF - 1);
         const double hr = hsel0[m].x, hi = hsel0[m].y;
         const double wr = post8192[b].x, wi = post8192[b].y;
         const double pr = 1.0 + wi, pi = -wr, qr = 1.0 - wi, qi = wr;   // 1 - i W, 1 + i W
-        c.x = (float)(hr * pr - hi * pi);
-        c.y = (float)(hr * pi + hi * pr);
-        c.z = (float)(hr * qr - hi * qi);
-        c.w = (float)(hr * qi + hi * qr);
+        if (b == HALF / 2) {   // P = 0: (Q, 0)
+            c.x = (float)(hr * qr - hi * qi);
+            c.y = (float)(hr * qi + hi * qr);
+        } else {
+            c.x = (float)(hr * pr - hi * pi);
+            c.y = (float)(hr * pi + hi * pr);
+            // r = Re[(1 + i W) / (i (1 - i W))] = Re[(qr + i qi) / (-pi + i pr)]
+            c.z = (float)((-qr * pi + qi * pr) / (pi * pi + pr * pr));
+        }
     }
-    pqf[i] = c;
+    float *const e = reinterpret_cast<float *>(pqf) + 3 * i;
+    e[0] = c.x;
+    e[1] = c.y;
+    e[2] = c.z;
     if (i < NT) {
         fsl[i] = tw4096[(tunebin * i) & (HALF - 1)];
         fsl[NT + i] = tw4096[((tunebin - 1) * i) & (HALF - 1)];

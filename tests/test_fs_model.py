@@ -97,10 +97,13 @@ def test_inplace_layout_bank_conflicts():
             assert _conflicts(ls[:, r], 32) == 0, (name, "ld", r)
 
 
+@pytest.mark.parametrize("split", ["pq", "pr"])
 @pytest.mark.parametrize("tb", [0, 4, 284, 1024, 1228, 2048, 3888, 4092])
-def test_fs_model_matches_oracle(tb):
+def test_fs_model_matches_oracle(tb, split):
+    """both forms of the split x filter: Z P + conj(Zc) Q (round 5) and P (Z + i r conj(Zc)) with
+    the real ratio r = Q / (i P) (round 6, the kernel's: 12 table bytes per bin, 6 VALU)"""
     perm = np.array(P.read_header())
     H = O.filter_bank(1.0)[0]
     x = make_stream(1, "mix")
-    y = M.r2iq_fs(x, 1, tb, H, perm)
+    y = M.r2iq_fs(x, 1, tb, H, perm, split)
     assert O.max_rel_err(y, O.r2iq(x, 1, 0, tb)) < 1e-12

@@ -25,8 +25,10 @@ def dft16(a, sign):
     return a @ M
 
 
-def frame_fs(x8192, tb, H, perm):
-    """one d = 0 frame: 8192 real samples -> 4096 complex outputs (before overlap-discard)"""
+def frame_fs(x8192, tb, H, perm, split="pr"):
+    """one d = 0 frame: 8192 real samples -> 4096 complex outputs (before overlap-discard).
+    split "pq": F = Z P + conj(Zc) Q (round 5); "pr" (round 6): Q = i r P with r real, so
+    F = P (Z + i r conj(Zc)), except the bin 2048 (column 0, register 8: P = 0), F = Q conj(Z)"""
     z = x8192[0::2] + 1j * x8192[1::2]
     t = np.arange(256)
     # F0: butterfly t, inputs z[t + 256 r], out pos 16 t + k
@@ -59,7 +61,17 @@ def frame_fs(x8192, tb, H, perm):
     zc[0] = Zl[0][(16 - r) % 16]
     zc[1] = Zl[1][15 - r]
     assert np.allclose(zc, Z[(-beta) % HALF])
-    F = Zl * P + np.conj(zc) * Q
+    if split == "pq":
+        F = Zl * P + np.conj(zc) * Q
+    else:
+        # r = Q / (i P) = (1 + i W) / (i (1 - i W)) = cot(pi/4 - pi beta / 8192): real, tune-bin and
+        # filter independent; infinite only at beta = 2048 (lane 0, register 8)
+        sp = (beta == 2048)
+        with np.errstate(divide="ignore", invalid="ignore"):
+            rr = np.where(sp, 0.0, ((1 + 1j * Wb) / (1j * (1 - 1j * Wb))).real)
+        assert np.allclose(np.where(sp | ~valid, 0, Q - 1j * rr * P), 0, atol=1e-12 * np.abs(Q).max())
+        F = P * (Zl + 1j * rr * np.conj(zc))
+        F[sp] = Q[sp] * np.conj(Zl[sp])
     # I0 (NS = 1): butterfly c, inputs F[c + 256 s], out pos 16 c + k
     C = np.empty(HALF, complex)
     o = dft16(F, +1)
@@ -81,12 +93,12 @@ def frame_fs(x8192, tb, H, perm):
     return y
 
 
-def r2iq_fs(stream, nblk, tb, H, perm):
+def r2iq_fs(stream, nblk, tb, H, perm, split="pr"):
     out = np.empty(nblk * 32768, complex)
     for b in range(nblk):
         for k in range(FRAMES):
             s = b * BLOCK + k * HOP
-            y = frame_fs(stream[s:s + 2 * HALF].astype(np.float64), tb, H, perm)
+            y = frame_fs(stream[s:s + 2 * HALF].astype(np.float64), tb, H, perm, split)
             if k == 0:
                 out[b * 32768: b * 32768 + 2048] = y[1024:3072]
             else:
