@@ -151,6 +151,15 @@ __device__ __forceinline__ void wg_pass(const float2 *src, float2 *dst, const fl
     }
 }
 
+// element e of a tail buffer, with e = lane ^ R for bits of lane and R that do not overlap: the
+// swizzle is linear over XOR (tail_swz(a ^ b) = tail_swz(a) ^ tail_swz(b)), so the byte offset is
+// (8 tail_swz(lane)) ^ (8 tail_swz(R)), one v_xor_b32 with an immediate per access (as lds_x)
+template <int N>
+__device__ __forceinline__ float2 &tail_x(float2 *buf, unsigned lane8, int R)
+{
+    return *reinterpret_cast<float2 *>(reinterpret_cast<char *>(buf) + (lane8 ^ (8u * (unsigned)tail_swz<N>(R))));
+}
+
 template <int N, int P>
 __device__ __forceinline__ void tail_pass(float2 *sb, const float2 *twq, int t, float2 (&u)[8])
 {
@@ -158,8 +167,10 @@ __device__ __forceinline__ void tail_pass(float2 *sb, const float2 *twq, int t, 
     const int kk = t & (NS - 1);
     if (t < T) {
         float2 a[R];
+        // reads t + T r: t < T, so the two terms share no bit
+        const unsigned rd8 = 8u * (unsigned)tail_swz<N>(t);
 #pragma unroll
-        for (int r = 0; r < R; r++) a[r] = sb[tail_swz<N>(t + T * r)];
+        for (int r = 0; r < R; r++) a[r] = tail_x<N>(sb, rd8, T * r);
         if constexpr (P > 0) {
 #pragma unroll
             for (int r = 1; r < R; r++) a[r] = TW<+1>(a[r], twq[tail_twoff<N>(P) + (r - 1) * NS + kk]);
@@ -170,8 +181,10 @@ __device__ __forceinline__ void tail_pass(float2 *sb, const float2 *twq, int t, 
     if constexpr (P + 1 < tail_passes<N>()) {
         wave_lds_sync();   // this wave's reads of the pass are done
         if (t < T) {
+            // writes (t / NS) R NS + kk + NS r: kk < NS, NS r < R NS, so again disjoint bits
+            const unsigned wr8 = 8u * (unsigned)tail_swz<N>((t / NS) * R * NS + kk);
 #pragma unroll
-            for (int r = 0; r < R; r++) sb[tail_swz<N>((t / NS) * R * NS + kk + NS * r)] = u[r];
+            for (int r = 0; r < R; r++) tail_x<N>(sb, wr8, NS * r) = u[r];
         }
         wave_lds_sync();
     }
@@ -214,15 +227,17 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
     constexpr bool ZROT = !PRUNE;
     const int zd = tunebin & 255;
     const int mrel = ((((1 - s0 - N) & (HALF - 1)) >> 8) - r0) & 15;
-    // d >= 5: the pruned pass 2 keeps registers {0, 1, mrel, mrel + 1}, i.e. the DFT-16 output
-    // groups k1 = r & 3 in {0, 1, mrel & 3, (mrel + 1) & 3}; groups 2, 3 are computed only when
-    // the mirror needs them (dft16_groups, uniform flags): d = 5, 6 +1-2.8 % (tb 192 / 1024),
-    // bit-identical, d = 4 unchanged (profiles/r02/ab/grp5_d5_6*.txt).  At
-    // d = 4 the branches raise the kernel to 142 VGPRs (3 waves/SIMD, 9-13 % slower; held to 128
-    // it spills), so d = 4 keeps dft16 (profiles/r02/ab/grp_partial_dft16*.txt).
-    // (round 4: re-measured at d = 4 after the tails and the queue's removal left it at 90 VGPRs:
-    // 111 VGPRs, still 4 waves/SIMD, +4 %, profiles/r04/ab/pruned_f2_d4.txt; so d >= 4)
-    constexpr bool GRP = PRUNE && NB == 2 && D >= 4;
+    // The pruned pass 2 computes only the DFT-16 outputs it stores: registers 0 .. NB - 1 and
+    // mrel .. mrel + NB - 1 (mod 16), dft16_need with a wave-uniform mask (output pairs r, r + 8
+    // skipped when both are unneeded, first-stage halves with them): 10 of 16 outputs at d = 2,
+    // 6 at d = 3, 4 at d >= 4.  Rounds 2-5 pruned only whole k1 groups and only at d >= 4
+    // (dft16_groups: d = 5, 6 +1-2.8 %, d = 4 +4 %, profiles/r02/ab/grp5_d5_6*.txt,
+    // profiles/r04/ab/pruned_f2_d4.txt); round 6 (profiles/r06/ab/persistent_f2_need_*.txt).  At
+    // d = 5, 6 dft16_need takes the kernel past 128 VGPRs (137 / 129: 3 waves per SIMD), so they
+    // keep the k1-group form.
+    constexpr bool NEED = PRUNE && D <= 4, GRP = PRUNE && D >= 5;
+    const unsigned nbm = (1u << NB) - 1u;
+    const unsigned need = __builtin_amdgcn_readfirstlane((nbm | (nbm << mrel) | (nbm >> (16 - mrel))) & 0xffffu);
     const bool need2 = ((mrel & 3) - 1u) <= 1u, need3 = (mrel & 3) >= 2;
     __shared__ __attribute__((aligned(16))) float2 lds[HALF];
     // pass-1 twiddle tables, copied once per workgroup: [15][16] forward, [15][S] inverse
@@ -386,7 +401,8 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
 #pragma unroll
             for (int r = 0; r < 16; r++) XRD(a[r], w1[sT + NT * r]);
             twiddle_anchor6<-1>(a, fw1, fw2, fw3, fw4, fw8, fw12);
-            if constexpr (GRP) dft16_groups<-1>(a, v, need2, need3);
+            if constexpr (NEED) dft16_need<-1>(a, v, need);
+            else if constexpr (GRP) dft16_groups<-1>(a, v, need2, need3);
             else dft16<-1>(a, v);
         }
         ST_SYNC(4);

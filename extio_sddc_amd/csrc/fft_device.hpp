@@ -275,6 +275,67 @@ __device__ __forceinline__ void dft16_groups(const float2 *v, float2 *o, bool ne
     }
 }
 
+// dft16 computing only the outputs the wave-uniform mask `need` asks for (bit r: o[r]), at the
+// granularity of dft16's output pairs (k1 + 4h, k1 + 4h + 8), h = 0, 1: the first stage's
+// radix-4 halves and the second stage's pair computations whose outputs are all unneeded are
+// skipped.  Every computed output takes dft16's operations in dft16's order (bit-identical); the
+// others are left unwritten.  Used where the caller keeps a few bins of the transform (the
+// persistent kernel's pruned forward pass 2 at d >= 2: 10 of 16 outputs at d = 2, 6 at d = 3,
+// 4 at d >= 4).
+template <int DIR>
+__device__ __forceinline__ void dft16_need(const float2 *v, float2 *o, unsigned need)
+{
+    constexpr float kT1 = 0.41421356237309504880f;
+    constexpr float kT3 = 2.41421356237309504880f;
+    // pair (k1, h): outputs k1 + 4 h and k1 + 4 h + 8
+    const bool p00 = need & 0x0101u, p01 = need & 0x1010u, p10 = need & 0x0202u, p11 = need & 0x2020u;
+    const bool p20 = need & 0x0404u, p21 = need & 0x4040u, p30 = need & 0x0808u, p31 = need & 0x8080u;
+    const bool g0 = p00 || p01, g1 = p10 || p11, g2 = p20 || p21, g3 = p30 || p31;
+    float2 b[4][4];  // b[n2][k1]
+#pragma unroll
+    for (int n2 = 0; n2 < 4; n2++) {
+        if (g0 || g2) {
+            const float2 t0 = cadd(v[n2], v[8 + n2]), t2 = cadd(v[4 + n2], v[12 + n2]);
+            if (g0) b[n2][0] = cadd(t0, t2);
+            if (g2) b[n2][2] = csub(t0, t2);
+        }
+        if (g1 || g3) {
+            const float2 t1 = csub(v[n2], v[8 + n2]), t3 = mulj<DIR>(csub(v[4 + n2], v[12 + n2]));
+            if (g1) b[n2][1] = cadd(t1, t3);
+            if (g3) b[n2][3] = csub(t1, t3);
+        }
+    }
+    if (p00) {   // k1 = 0: dft4 over n2
+        const float2 t0 = cadd(b[0][0], b[2][0]), t2 = cadd(b[1][0], b[3][0]);
+        o[0] = cadd(t0, t2);
+        o[8] = csub(t0, t2);
+    }
+    if (p01) {
+        const float2 t1 = csub(b[0][0], b[2][0]), t3 = mulj<DIR>(csub(b[1][0], b[3][0]));
+        o[4] = cadd(t1, t3);
+        o[12] = csub(t1, t3);
+    }
+    float2 t0, t1, p, q;
+    if (g1) {   // k1 = 1 (as dft16)
+        axpm(b[0][1], kR2, rot1(b[2][1], (float)DIR), t0, t1);
+        axpm(rot1(b[1][1], DIR * kT1), kT1, rot1(b[3][1], DIR * kT3), p, q);
+        if (p10) axpm(t0, kC16_1, p, o[1], o[9]);
+        if (p11) ajpm<DIR>(t1, kC16_1, q, o[5], o[13]);
+    }
+    if (g2) {   // k1 = 2
+        ajpm<DIR>(b[0][2], 1.f, b[2][2], t0, t1);
+        axpm(rot1(b[1][2], (float)DIR), -1.f, rot1(b[3][2], (float)-DIR), p, q);
+        if (p20) axpm(t0, kR2, p, o[2], o[10]);
+        if (p21) ajpm<DIR>(t1, kR2, q, o[6], o[14]);
+    }
+    if (g3) {   // k1 = 3
+        axpm(b[0][3], -kR2, rot1(b[2][3], (float)-DIR), t0, t1);
+        axpm(rot1(b[1][3], DIR * kT3), -kT3, rot1(b[3][3], DIR * kT1), p, q);
+        if (p30) axpm(t0, kS16_1, p, o[3], o[11]);
+        if (p31) ajpm<DIR>(t1, kS16_1, q, o[7], o[15]);
+    }
+}
+
 // a[r] *= W^{r} for r = 1..15 given the forward-direction W^1 and W^4 of this lane
 // (conjugated for DIR = +1).
 // p = A w, m = A conj(w) for a unit w
