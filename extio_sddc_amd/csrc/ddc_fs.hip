@@ -126,6 +126,11 @@ __device__ __forceinline__ void emit_frame_q(void *__restrict__ out, int fbase, 
 
 // The queue wave (not wave 0, which also carries the self-mirrored columns' split)
 constexpr int kQWave = 3;
+// (P, r) table loads in flight ahead of the split's use, in bin pairs (p, 15 - p).  Two pairs
+// (113 VGPRs since the 12-byte table) measured 1 % slower (profiles/r06/ab/fs_pq_ahead2_*.txt);
+// holding forward pass 2's eight product twiddle powers in registers across frames (26 VALU per
+// wave-frame fewer, 128 VGPRs, spills in the NCO / CS16 instances) measured neutral (same files).
+constexpr int kFsPqAhead = 1;
 // fs_slot(t, 0): the F0 / I2 row of thread t
 __device__ __forceinline__ int fs_row_slot(int t) { return 272 * (t >> 4) + (t >= 128) + 34 * ((t & 15) >> 1) + (t & 1); }
 // fs_pair_lane: F1's and I1's thread t takes row u = 2 (t >> 5) + (t & 1) of each 16-row block,
@@ -303,12 +308,15 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
         // The split's (P, r) loads (bin pairs p, 15 - p; 12 bytes per bin) run a pair ahead of
         // their use, the first issued before F2 so that its reads and arithmetic cover the L2
         // latency (an empty asm with a memory clobber pins each group; the compiler's own schedule
-        // waits for every pair right after issuing it).  Two pairs ahead of F2 spill at 128 VGPRs.
+        // waits for every pair right after issuing it).
         const __amdgpu_buffer_rsrc_t rpq = buf_rsrc(pqf + z);
         const unsigned t12 = 12u * (unsigned)t;
         float3 qa[8], qb[8];
-        if constexpr (!zrow<ZR>(0)) qa[0] = buf_load12(rpq, t12, 0);
-        if constexpr (!zrow<ZR>(15)) qb[0] = buf_load12(rpq, t12, 12u * NT * 15);
+#pragma unroll
+        for (int p = 0; p < kFsPqAhead; p++) {
+            if (!zrow<ZR>(p)) qa[p] = buf_load12(rpq, t12, 12u * NT * p);
+            if (!zrow<ZR>(15 - p)) qb[p] = buf_load12(rpq, t12, 12u * NT * (15 - p));
+        }
         asm volatile("" ::: "memory");
         {
             float2 a[16];
@@ -334,9 +342,10 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
                 const int lane = t & 63;
 #pragma unroll
                 for (int p = 0; p < 8; p++) {
-                    if (p + 1 < 8) {
-                        if (!zrow<ZR>(p + 1)) qa[p + 1] = buf_load12(rpq, t12, 12u * NT * (p + 1));
-                        if (!zrow<ZR>(14 - p)) qb[p + 1] = buf_load12(rpq, t12, 12u * NT * (14 - p));
+                    if (p + kFsPqAhead < 8) {
+                        const int pn = p + kFsPqAhead;
+                        if (!zrow<ZR>(pn)) qa[pn] = buf_load12(rpq, t12, 12u * NT * pn);
+                        if (!zrow<ZR>(15 - pn)) qb[pn] = buf_load12(rpq, t12, 12u * NT * (15 - pn));
                         asm volatile("" ::: "memory");
                     }
 #pragma unroll
@@ -357,9 +366,10 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
             auto split_generic = [&]() __attribute__((always_inline)) {
 #pragma unroll
                 for (int p = 0; p < 8; p++) {
-                    if (p + 1 < 8) {
-                        if (!zrow<ZR>(p + 1)) qa[p + 1] = buf_load12(rpq, t12, 12u * NT * (p + 1));
-                        if (!zrow<ZR>(14 - p)) qb[p + 1] = buf_load12(rpq, t12, 12u * NT * (14 - p));
+                    if (p + kFsPqAhead < 8) {
+                        const int pn = p + kFsPqAhead;
+                        if (!zrow<ZR>(pn)) qa[pn] = buf_load12(rpq, t12, 12u * NT * pn);
+                        if (!zrow<ZR>(15 - pn)) qb[pn] = buf_load12(rpq, t12, 12u * NT * (15 - pn));
                         asm volatile("" ::: "memory");
                     }
                     if (zrow<ZR>(15 - p)) {   // row 15 - p zero: row p's bin alone (v[15 - p] unwritten)
