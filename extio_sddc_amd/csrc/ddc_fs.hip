@@ -560,7 +560,7 @@ hipError_t launch_fs_s(const KernelTables &t, const int16_t *d_in, int nblk, voi
     int grid = cus * occ;
     if (grid > nframes) grid = nframes;
     int ns = frame_schedule_static(nframes, static_pct);
-    unsigned slotw = occ == 4 && grid == cus * occ ? kFsSlotWeights : 0u;
+    unsigned slotw = occ == 4 && grid == cus * occ ? (fs.slotw ? fs.slotw : kFsSlotWeights) : 0u;
     int xmap = 0;
     if (fpw > 0) {   // non-persistent: fpw frames per workgroup, the hardware dispatcher balances
         grid = (nframes + fpw - 1) / fpw;

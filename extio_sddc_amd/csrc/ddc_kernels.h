@@ -113,6 +113,7 @@ struct FsSched {
     int minrem = 1;
     int pub = 0;   // frames at the end of each range open to thieves (0: all but the first two)
     int zr = 1;    // skip the tune bin's whole zero rows of the inverse input (0: never; A/B)
+    unsigned slotw = 0u;   // the static split's slot weights (slot_weights4 packing); 0: kFsSlotWeights
 };
 hipError_t launch_frames_fs(const KernelTables &t, const int16_t *d_in, int nblk, void *d_out, const float4 *pqf,
                             const float2 *fsl, int tunebin, int lsb, int rand, int cs16, float cs16_scale,

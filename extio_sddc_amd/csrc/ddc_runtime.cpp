@@ -735,6 +735,14 @@ int sddc_ddc_internal_set_param(sddc_ddc_t *h, int param, int value)
     case SDDC_DDC_PARAM_FS_ZERO_ROWS:
         h->fs_sched.zr = value != 0;
         return SDDC_OK;
+    case SDDC_DDC_PARAM_FS_SLOT_WEIGHTS: {
+        for (int k = 0; k < 4 && value != 0; k++) {
+            const int wk = (value >> (8 * k)) & 0xff;
+            if (wk < 1 || wk > 127) return fail(SDDC_ERR_ARG, "slot weight %d of slot %d outside 1..127", wk, k);
+        }
+        h->fs_sched.slotw = (unsigned)value;
+        return SDDC_OK;
+    }
     case SDDC_DDC_PARAM_FS_STEAL_PUBLIC:
         if (value < 0 || value > 1024) return fail(SDDC_ERR_ARG, "public frames %d outside 0..1024", value);
         h->fs_sched.pub = value;

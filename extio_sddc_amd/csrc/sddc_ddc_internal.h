@@ -30,6 +30,10 @@ extern "C" {
  * 4 rows or none for the fused-NCO and CS16 outputs and the queue / stealing schedules; a single
  * zero row is computed); 0: computes them all (A/B, tests). */
 #define SDDC_DDC_PARAM_FS_ZERO_ROWS 7
+/* SDDC_DDC_PARAM_FS_SLOT_WEIGHTS: the d = 0 kernel's slot weights of the static split, four
+ * bytes w0 | w1 << 8 | w2 << 16 | w3 << 24 (CU slot 0 in the low byte, each 1..127); 0: the
+ * built-in kFsSlotWeights (A/B of the weights). */
+#define SDDC_DDC_PARAM_FS_SLOT_WEIGHTS 8
 
 int sddc_ddc_internal_set_param(sddc_ddc_t *h, int param, int value);
 /* Diagnostic stamp buffers of -DSDDC_STAMPS builds (tools/fs_stamps.py); -1 in product builds. */
