@@ -691,18 +691,6 @@ def main() -> None:
                           "launch duration, from the same steps on one stream"}
         kern_ms = kern1
 
-    # single mode: every rank checks its segment (the halo'd first block, a middle block) against
-    # a separate launch over a window starting a block earlier; max error / all identical over ranks
-    seg_check = None
-    if args.mode == "single" and not (args.cs16 or args.fine_tune):
-        seg_check = segment_check(torch, ddc, d, nblk, rank, dev, stream, pouts[0])
-        if world > 1:
-            tt = torch.tensor([seg_check["max_rel_err"], 0.0 if seg_check["bit_identical"] else 1.0],
-                              dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            seg_check = {"ranks": world, "blocks_checked_rank0": seg_check["blocks_checked"],
-                         "max_rel_err_over_ranks": tt[0].item(), "bit_identical_all_ranks": tt[1].item() == 0.0}
-
     # N > 1 channels: the collective and the compute, each timed alone (max over ranks), so the
     # line shows which of the two bounds the pipelined step
     bcast_info = None
@@ -737,6 +725,20 @@ def main() -> None:
         ddc.updateRand(False)
         ddc.process_device(d_in, nblk, d_out, stream)   # d_out holds the headline config again
         torch.cuda.synchronize()
+
+    # single mode: every rank checks its segment (the halo'd first block, a middle block) against
+    # a separate launch over a window starting a block earlier; max error / all identical over ranks.
+    # After the sweep: its host round trips idle the GPU, and the sweep's first config (d = 0) would
+    # then run on a clock still ramping back up
+    seg_check = None
+    if args.mode == "single" and not (args.cs16 or args.fine_tune):
+        seg_check = segment_check(torch, ddc, d, nblk, rank, dev, stream, d_out)
+        if world > 1:
+            tt = torch.tensor([seg_check["max_rel_err"], 0.0 if seg_check["bit_identical"] else 1.0],
+                              dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            seg_check = {"ranks": world, "blocks_checked_rank0": seg_check["blocks_checked"],
+                         "max_rel_err_over_ranks": tt[0].item(), "bit_identical_all_ranks": tt[1].item() == 0.0}
 
     value = samples_per_step_all * args.steps / wall / 1e6
     # roofline of the dominant kernel on THIS rank's launch

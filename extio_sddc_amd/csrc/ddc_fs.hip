@@ -56,7 +56,8 @@ __device__ __forceinline__ float dpp_partner(float v)
     return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, true));
 }
 
-// The split x filter of bin b from the table entry (P, r), r = Q / (i P) real (below):
+// The split x filter of bin b from P (the per-tune-bin table) and r = Q / (i P) (real, tune-bin
+// independent, held in registers; build_fs_tables_kernel):
 //   F = Z_b P + conj(Z_-b) Q = P (Z_b + i r conj(Z_-b)),   Z_b + i r conj(Z_-b) = (Z.x + r Zm.y, Z.y + r Zm.x)
 // with Z_-b the partner lane's register 15 - k: the DPP operand of two FMAs (v_fmac_f32_dpp), then
 // the product with P.  s_nop 1: a DPP read of a VGPR needs two wait states after the VALU write
@@ -85,17 +86,10 @@ __device__ __forceinline__ void split_v1(float2 &z, float2 zp, float r)
         : "v"(zp.x), "v"(zp.y), "v"(r));
 }
 
-// F = P V for the table entry q = (P.x, P.y, r)
-__device__ __forceinline__ float2 p_mul(float2 v, float3 q)
+// F = P V
+__device__ __forceinline__ float2 p_mul(float2 v, float2 q)
 {
     return make_float2(fmaf(v.x, q.x, -v.y * q.y), fmaf(v.x, q.y, v.y * q.x));
-}
-
-__device__ __forceinline__ float3 buf_load12(__amdgpu_buffer_rsrc_t r, unsigned voff, unsigned soff)
-{
-    typedef unsigned u32x3 __attribute__((ext_vector_type(3)));
-    const u32x3 v = __builtin_amdgcn_raw_buffer_load_b96(r, voff, soff, 0);
-    return make_float3(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z));
 }
 
 // v (-i)^s, then the sideband flip (imag sign) when LSB: s and LSB are constants after unrolling,
@@ -126,8 +120,8 @@ __device__ __forceinline__ void emit_frame_q(void *__restrict__ out, int fbase, 
 
 // The queue wave (not wave 0, which also carries the self-mirrored columns' split)
 constexpr int kQWave = 3;
-// (P, r) table loads in flight ahead of the split's use, in bin pairs (p, 15 - p).  Two pairs
-// (113 VGPRs since the 12-byte table) measured 1 % slower (profiles/r06/ab/fs_pq_ahead2_*.txt);
+// P table loads in flight ahead of the split's use, in bin pairs (p, 15 - p).  Two pairs
+// (113 VGPRs with the 12-byte (P, r) table) measured 1 % slower (profiles/r06/ab/fs_pq_ahead2_*.txt);
 // holding forward pass 2's eight product twiddle powers in registers across frames (26 VALU per
 // wave-frame fewer, 128 VGPRs, spills in the NCO / CS16 instances) measured neutral (same files).
 constexpr int kFsPqAhead = 1;
@@ -235,6 +229,28 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
     // on the queue wave and the next frame through s_next (the queue: every frame; work stealing:
     // the range's public end and what it steals).  Phase A is a copy of the frame body without
     // the schedule's registers, so the owner's frames cost what the static schedule's do.
+    // Frame-invariant lane values held in registers for the whole launch (read once here instead
+    // of from L2 every frame): the split's r of the lane's live bins (16 - |ZR| VGPRs; the P table
+    // drops to 8 bytes per bin) and, for the static schedule, I2's lane factors g_t, g_t W^{-t},
+    // g_t W^{-4t} (6 VGPRs; the queue and stealing schedules, at 124-128 VGPRs, keep the loads).
+    // Per frame 12 KB of table reads fewer at tb = 1024: +2.5-3 % (profiles/r06/ab/
+    // fs_cached_r_and_lane_factors_*.txt).  118 VGPRs at ZR = 4.
+    float cr[16];
+    {
+        const __amdgpu_buffer_rsrc_t rr = buf_rsrc(reinterpret_cast<const float *>(pqf) + 2 * HALF);
+#pragma unroll
+        for (int k = 0; k < 16; k++)
+            if (!zrow<ZR>(k)) cr[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rr, 4u * tid, 4u * NT * k, 0));
+    }
+    constexpr bool GREG = SCHED == kSchedStatic;
+    float2 cg0, cg1, cg4;
+    if constexpr (GREG) {
+        const __amdgpu_buffer_rsrc_t rfs = buf_rsrc(fsl);
+        const unsigned t8 = 8u * (unsigned)tid;
+        cg0 = buf_load8(rfs, t8, 0);
+        cg1 = buf_load8(rfs, t8, 8u * NT);
+        cg4 = buf_load8(rfs, t8, 16u * NT);
+    }
     int pA = -1, fend = -1;
     {
         const int G = (int)gridDim.x, a = slot_split(ns, G, w, slotw), b = slot_split(ns, G, w + 1, slotw);
@@ -305,17 +321,17 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
         if constexpr (PB && SCHED == kSchedSteal)
             if (qw) fsch.peek();
         // ---- F2 (R16, NS256) on column c: Z[c + 256 k] in v[k] ----
-        // The split's (P, r) loads (bin pairs p, 15 - p; 12 bytes per bin) run a pair ahead of
-        // their use, the first issued before F2 so that its reads and arithmetic cover the L2
-        // latency (an empty asm with a memory clobber pins each group; the compiler's own schedule
-        // waits for every pair right after issuing it).
+        // The split's P loads (bin pairs p, 15 - p; 8 bytes per bin) run a pair ahead of their
+        // use, the first issued before F2 so that its reads and arithmetic cover the L2 latency
+        // (an empty asm with a memory clobber pins each group; the compiler's own schedule waits
+        // for every pair right after issuing it).
         const __amdgpu_buffer_rsrc_t rpq = buf_rsrc(pqf + z);
-        const unsigned t12 = 12u * (unsigned)t;
-        float3 qa[8], qb[8];
+        const unsigned t8p = 8u * (unsigned)t;
+        float2 qa[8], qb[8];
 #pragma unroll
         for (int p = 0; p < kFsPqAhead; p++) {
-            if (!zrow<ZR>(p)) qa[p] = buf_load12(rpq, t12, 12u * NT * p);
-            if (!zrow<ZR>(15 - p)) qb[p] = buf_load12(rpq, t12, 12u * NT * (15 - p));
+            if (!zrow<ZR>(p)) qa[p] = buf_load8(rpq, t8p, 8u * NT * p);
+            if (!zrow<ZR>(15 - p)) qb[p] = buf_load8(rpq, t8p, 8u * NT * (15 - p));
         }
         asm volatile("" ::: "memory");
         {
@@ -344,20 +360,20 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
                 for (int p = 0; p < 8; p++) {
                     if (p + kFsPqAhead < 8) {
                         const int pn = p + kFsPqAhead;
-                        if (!zrow<ZR>(pn)) qa[pn] = buf_load12(rpq, t12, 12u * NT * pn);
-                        if (!zrow<ZR>(15 - pn)) qb[pn] = buf_load12(rpq, t12, 12u * NT * (15 - pn));
+                        if (!zrow<ZR>(pn)) qa[pn] = buf_load8(rpq, t8p, 8u * NT * pn);
+                        if (!zrow<ZR>(15 - pn)) qb[pn] = buf_load8(rpq, t8p, 8u * NT * (15 - pn));
                         asm volatile("" ::: "memory");
                     }
 #pragma unroll
                     for (int h = 0; h < 2; h++) {
                         const int kk = h ? 15 - p : p;
                         if (zrow<ZR>(kk)) continue;
-                        const float3 q = h ? qb[p] : qa[p];
+                        const float2 q = h ? qb[p] : qa[p];
                         const float2 vm = v[15 - kk], v0m = v[(16 - kk) & 15];
                         float2 zc = make_float2(dpp_partner(vm.x), dpp_partner(vm.y));
                         zc = lane == 1 ? vm : zc;
                         zc = lane == 0 ? v0m : zc;
-                        float2 vv = make_float2(fmaf(q.z, zc.y, v[kk].x), fmaf(q.z, zc.x, v[kk].y));
+                        float2 vv = make_float2(fmaf(cr[kk], zc.y, v[kk].x), fmaf(cr[kk], zc.x, v[kk].y));
                         if (kk == 8) vv = lane == 0 ? make_float2(v[8].x, -v[8].y) : vv;
                         a[kk] = p_mul(vv, q);
                     }
@@ -368,19 +384,19 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
                 for (int p = 0; p < 8; p++) {
                     if (p + kFsPqAhead < 8) {
                         const int pn = p + kFsPqAhead;
-                        if (!zrow<ZR>(pn)) qa[pn] = buf_load12(rpq, t12, 12u * NT * pn);
-                        if (!zrow<ZR>(15 - pn)) qb[pn] = buf_load12(rpq, t12, 12u * NT * (15 - pn));
+                        if (!zrow<ZR>(pn)) qa[pn] = buf_load8(rpq, t8p, 8u * NT * pn);
+                        if (!zrow<ZR>(15 - pn)) qb[pn] = buf_load8(rpq, t8p, 8u * NT * (15 - pn));
                         asm volatile("" ::: "memory");
                     }
                     if (zrow<ZR>(15 - p)) {   // row 15 - p zero: row p's bin alone (v[15 - p] unwritten)
-                        split_v1(v[p], v[15 - p], qa[p].z);
+                        split_v1(v[p], v[15 - p], cr[p]);
                         a[p] = p_mul(v[p], qa[p]);
                     } else if (zrow<ZR>(p)) {
-                        split_v1(v[15 - p], v[p], qb[p].z);
+                        split_v1(v[15 - p], v[p], cr[15 - p]);
                         a[15 - p] = p_mul(v[15 - p], qb[p]);
                     } else {
                         float2 vb = v[15 - p];
-                        split_v2(v[p], vb, v[15 - p], qa[p].z, qb[p].z);
+                        split_v2(v[p], vb, v[15 - p], cr[p], cr[15 - p]);
                         a[p] = p_mul(v[p], qa[p]);
                         a[15 - p] = p_mul(vb, qb[p]);
                     }
@@ -423,7 +439,16 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
         // table): issued ahead of the input prefetch, so that their wait does not include it
         const __amdgpu_buffer_rsrc_t rfs = buf_rsrc(fsl);
         const unsigned t8 = 8u * (unsigned)t;
-        const float2 g0 = buf_load8(rfs, t8, 0), g1 = buf_load8(rfs, t8, 8u * NT), g4 = buf_load8(rfs, t8, 16u * NT);
+        float2 g0, g1, g4;
+        if constexpr (GREG) {
+            g0 = cg0;
+            g1 = cg1;
+            g4 = cg4;
+        } else {
+            g0 = buf_load8(rfs, t8, 0);
+            g1 = buf_load8(rfs, t8, 8u * NT);
+            g4 = buf_load8(rfs, t8, 16u * NT);
+        }
         int fn;
         // ---- I1 (R16, NS16): table twiddles W_256^{-s r} ----
         {
@@ -500,14 +525,16 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
         if (tid == QLANE) fs_queue_done(wq, (unsigned)gridDim.x);
 }
 
-// FS tables of one tunebin: pqf[l + 256 k] = (P, r), 12 bytes, of bin b = kFsPerm[l] + 256 k
-// (inverse input m = (b - tb) mod 4096; P and Q = i r P zero unless b is in the reference's band:
+// FS tables of one tunebin, for lane l and row k (bin b = kFsPerm[l] + 256 k): P as float2 at
+// pqf[l + 256 k] (bytes 0 .. 32 K) and r as float at byte 32 K + 4 (l + 256 k) (inverse input
+// m = (b - tb) mod 4096; P and Q = i r P zero unless b is in the reference's band:
 // tb <= b < tb + 2048, b < 4096, or tb - 2048 <= b < tb).  With P = H (1 - i W), Q = H (1 + i W)
 // (H = H_0[m] / 2, W = e^{-2 pi i b / 8192}), r = Q / (i P) = (1 + i W) / (i (1 - i W))
 // = cot(pi/4 - pi b / 8192) is real and does not depend on H or the tune bin; it is infinite only
 // at b = 2048 (column 0, register 8), whose entry holds (Q, 0) instead (the kernel's wave-0 path).
-// Versus the (P, Q) float4 of round 5: 12 bytes per bin instead of 16 (the table is read from L2
-// every frame) and 6 or 7 VALU per bin instead of 8.  tools/fs_model.py (split "pr") models it.
+// Versus the (P, Q) float4 of round 5: 6 or 7 VALU per bin instead of 8, and 8 bytes per bin read
+// from L2 every frame instead of 16 (r is read once per launch).  tools/fs_model.py (split "pr")
+// models it.
 // fsl = [g_t | g_t W^{-t} | g_t W^{-4t}], g_t = e^{-2 pi i tb t / 4096}, looked up exactly in the
 // 4096-point table.
 __global__ void build_fs_tables_kernel(const float2 *__restrict__ hsel0, const float2 *__restrict__ post8192,
@@ -535,10 +562,8 @@ __global__ void build_fs_tables_kernel(const float2 *__restrict__ hsel0, const f
             c.z = (float)((-qr * pi + qi * pr) / (pi * pi + pr * pr));
         }
     }
-    float *const e = reinterpret_cast<float *>(pqf) + 3 * i;
-    e[0] = c.x;
-    e[1] = c.y;
-    e[2] = c.z;
+    reinterpret_cast<float2 *>(pqf)[i] = make_float2(c.x, c.y);
+    reinterpret_cast<float *>(pqf)[2 * HALF + i] = c.z;
     if (i < NT) {
         fsl[i] = tw4096[(tunebin * i) & (HALF - 1)];
         fsl[NT + i] = tw4096[((tunebin - 1) * i) & (HALF - 1)];
