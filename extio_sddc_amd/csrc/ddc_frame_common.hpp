@@ -44,13 +44,13 @@ __device__ __forceinline__ float2 TW(float2 a, float2 w) { return DIR < 0 ? cmul
 // reference's zero fill for out-of-band bins (impl.hpp:91-92, 95-96):
 //   X Hh = Hh [(Zk + conj Zc) - i W^bin (Zk - conj Zc)] = Zk P + conj(Zc) Q,
 //   P = Hh (1 - i W^bin),  Q = Hh (1 + i W^bin)     (Zc = Z[(4096 - bin) mod 4096])
-// from the per-(d, tunebin) table c = (P, Q) of build_split_filter_kernel, zero out of band.
-__device__ __forceinline__ float2 split_pq(float2 zk, float2 zc, float4 c)
+// Q = i r P with r = Q / (i P) = cot(pi/4 - pi bin / 8192) real (independent of H and the tune
+// bin), so X Hh = P (Zk + i r conj Zc) = P (Zk.x + r Zc.y, Zk.y + r Zc.x): 6 VALU and a float2
+// of P per bin (build_split_filter_kernel; r held in registers where the kernel has them).
+__device__ __forceinline__ float2 split_pr(float2 zk, float2 zc, float2 p, float r)
 {
-    float2 v;
-    v.x = zk.x * c.x - zk.y * c.y + zc.x * c.z + zc.y * c.w;
-    v.y = zk.x * c.y + zk.y * c.x + zc.x * c.w - zc.y * c.z;
-    return v;
+    const float vx = fmaf(r, zc.y, zk.x), vy = fmaf(r, zc.x, zk.y);
+    return make_float2(fmaf(vx, p.x, -vy * p.y), fmaf(vx, p.y, vy * p.x));
 }
 
 // Frame k of a block: output base of the kept samples, relative to the block's output

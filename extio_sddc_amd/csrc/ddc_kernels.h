@@ -65,7 +65,8 @@ struct KernelTables {
 };
 
 // v2 (default): persistent workgroups, input prefetch, swizzled LDS.  pq: the split x filter
-// coefficients of (d, tunebin), HALF >> d float4, built by launch_build_split_filter.
+// coefficients of (d, tunebin) built by launch_build_split_filter: N = HALF >> d float2 P, then N
+// float r (12 N bytes of the HALF float4 allocation).
 // nco_starts/nco_trig: fused fine-tune NCO tables (fine_tune.h), or nullptr for none.
 // cs16: write saturate(rint(x * cs16_scale)) int16 (I, Q) pairs instead of complex float.
 hipError_t launch_frames_persistent(const KernelTables &t, int d, const int16_t *d_in, int nblk,

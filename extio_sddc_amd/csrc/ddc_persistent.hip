@@ -15,7 +15,8 @@
 //     64-consecutive reads are bank-conflict free;
 //   * twiddles: small [r][s] tables copied to LDS once per workgroup for the NS <= 16 passes,
 //     a register recurrence from per-thread W^j, W^{4j} for the NS = 256 passes; the r2c split
-//     twiddle and the filter are one (P, Q) float4 per inverse input (build_split_filter_kernel).
+//     twiddle and the filter are P (a float2 per inverse input) and the real r = Q / (i P), held in
+//     registers at d >= 1 (split_pr, build_split_filter_kernel).
 // The measured-slower layouts, the first-generation kernels and the timing-only builds of the
 // A/B study are in git history (DESIGN.md §8 keeps their numbers).
 #include <hip/hip_runtime.h>
@@ -191,7 +192,7 @@ __device__ __forceinline__ void tail_pass(float2 *sb, const float2 *twq, int t, 
 }
 
 template <int D, bool RAND, bool NCO, bool CS16>
-__global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
+__global__ __launch_bounds__(NT, 4) void r2iq_persistent_kernel(
     const int *__restrict__ in32, void *__restrict__ out, int nframes,
     const float2 *__restrict__ tw_p1, const float2 *__restrict__ tw_q1,
     const float2 *__restrict__ rec_f, const float2 *__restrict__ rec_i, const float2 *__restrict__ tw4096,
@@ -318,6 +319,19 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
         }
     }
 
+    // d >= 2: the split's r of the thread's inverse inputs m = t + 256 r, held in registers for the
+    // launch (table reads per frame: the float2 P, 8 bytes per bin, instead of the (P, Q) float4's
+    // 16); d = 1 (126 VGPRs before; its 8 r spilled 12 VGPRs) and d = 0 (16 bins per thread)
+    // read r every frame, 12 bytes per bin
+    constexpr int RR = N >= 512 ? N / 256 : 1;
+    constexpr bool RREG = D >= 2;
+    float rreg[RR];
+    if constexpr (RREG) {
+        const float *rt = reinterpret_cast<const float *>(pq) + 2 * N;
+#pragma unroll
+        for (int r = 0; r < RR; r++) rreg[r] = (N >= 512 || tid < N) ? rt[tid + NT * r] : 0.f;
+    }
+
     __syncthreads();   // s_first, s_next
     int f = s_first;
     int fi = 0;                 // frames done by this workgroup (N <= 256: the slot in the batch of TB)
@@ -335,7 +349,7 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
         int z = 0;
         asm volatile("" : "+s"(z));
         const int t = tid + z;
-        const float4 *pqz = pq + z;
+        const float2 *pqz = reinterpret_cast<const float2 *>(pq) + z;   // P (split_pr)
         float2 fw1 = fw1_, fw4 = fw4_, iw1 = iw1_, iw4 = iw4_;
         asm volatile("" : "+v"(fw1), "+v"(fw4), "+v"(iw1), "+v"(iw4));
         float2 fw2 = fw2_, fw3 = fw3_, fw8 = fw8_, fw12 = fw12_;
@@ -429,8 +443,9 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
                 // mirror bin, same separability (rotated storage: HALF - b0 - tb)
                 const int sc0 = ZROT ? (HALF - b0 - tunebin) & (HALF - 1) : HALF - b0;   // (PRUNE: d = 2, 3)
                 const char *w0b = reinterpret_cast<const char *>(w0);
-                const unsigned sb0b = 8u * (unsigned)sb0, sc0b = 8u * (unsigned)sc0, tb16 = 16u * (unsigned)t;
+                const unsigned sb0b = 8u * (unsigned)sb0, sc0b = 8u * (unsigned)sc0, t8 = 8u * (unsigned)t;
                 const __amdgpu_buffer_rsrc_t rpq = buf_rsrc(pqz);
+                const __amdgpu_buffer_rsrc_t rrt = buf_rsrc(reinterpret_cast<const float *>(pqz) + 2 * N);
                 float2 a[R0];
 #pragma unroll
                 for (int r = 0; r < R0; r++) {
@@ -444,7 +459,8 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
                     else if constexpr (ZROT) zk = w0[t + (sh & (HALF - 1))];
                     else zk = *reinterpret_cast<const float2 *>(w0b + ((sb0b + 8u * (unsigned)sh) & (8u * HALF - 8u)));
                     const float2 zc = *reinterpret_cast<const float2 *>(w0b + ((sc0b - 8u * (unsigned)sh) & (8u * HALF - 8u)));
-                    a[r] = split_pq(zk, zc, buf_load16(rpq, tb16, 16u * NT * r));
+                    const float rv = RREG ? rreg[r] : __int_as_float(buf_load4(rrt, t8 >> 1, 4u * NT * r));
+                    a[r] = split_pr(zk, zc, buf_load8(rpq, t8, 8u * NT * r), rv);
                 }
                 if constexpr (WGT) {
                     constexpr int B = N / 1024, T = N / 4;
@@ -578,7 +594,7 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
             if (t < N) {
                 const int m = t;
                 const int bin = tunebin + m - (m >= N / 2 ? N : 0);
-                tv = split_pq(w0[bin & (HALF - 1)], w0[(HALF - bin) & (HALF - 1)], pqz[m]);
+                tv = split_pr(w0[bin & (HALF - 1)], w0[(HALF - bin) & (HALF - 1)], pqz[m], rreg[0]);
             }
             // The N filtered bins to sb, and the inverse as Stockham passes on one wave (the tail).
             // Frames go in batches of TB: frame j of a batch leaves its bins in sb[jN .. (j+1)N)
@@ -617,27 +633,37 @@ __global__ __launch_bounds__(NT, D <= 1 ? 4 : 2) void r2iq_persistent_kernel(
 }
 
 // ---------------------------------------------------------------------------------------------
-// Split x filter coefficients for one (d, tunebin): pq[m] = (P, Q) of inverse input m, with
-// bin = tb + m - (m >= N/2 ? N : 0) (fft_mt_r2iq_impl.hpp:84-98); zero outside [0, 4096).
-// Evaluated in double from the float tables and rounded once.
+// Split x filter coefficients for one (d, tunebin), inverse input m (bin = tb + m - (m >= N/2 ? N : 0),
+// fft_mt_r2iq_impl.hpp:84-98; zero outside [0, 4096)): P as float2 at pq[m] (bytes 0 .. 8 N) and
+// r = Q / (i P) as float at float index 2 N + m (split_pr).  r is infinite at bin 2048 (P = 0,
+// X Hh = Q conj Zc): there r = 2^64 and P = Q / (i 2^64), exact power-of-two scalings, so that
+// P (Zk + i r conj Zc) = Q conj Zc - i 2^-64 Q Zk, the second term far below float32's resolution
+// of the first (|Zc| < 2^28: no overflow).  Evaluated in double from the float tables and rounded once.
 __global__ void build_split_filter_kernel(const float2 *__restrict__ hsel, const float2 *__restrict__ post8192,
                                           int N, int tunebin, float4 *__restrict__ pq)
 {
     const int m = (int)(blockIdx.x * blockDim.x + threadIdx.x);
     if (m >= N) return;
     const int bin = tunebin + m - (m >= N / 2 ? N : 0);
-    float4 c = make_float4(0.f, 0.f, 0.f, 0.f);
+    float2 p = make_float2(0.f, 0.f);
+    float r = 0.f;
     if (bin >= 0 && bin < HALF) {
         const double hr = hsel[m].x, hi = hsel[m].y;
         const double wr = post8192[bin].x, wi = post8192[bin].y;
         // 1 - i W = (1 + wi, -wr), 1 + i W = (1 - wi, wr)
         const double pr = 1.0 + wi, pi = -wr, qr = 1.0 - wi, qi = wr;
-        c.x = (float)(hr * pr - hi * pi);
-        c.y = (float)(hr * pi + hi * pr);
-        c.z = (float)(hr * qr - hi * qi);
-        c.w = (float)(hr * qi + hi * qr);
+        if (bin == HALF / 2) {
+            constexpr double s = 0x1p-64;
+            const double q0 = hr * qr - hi * qi, q1 = hr * qi + hi * qr;
+            p = make_float2((float)(q1 * s), (float)(-q0 * s));   // -i Q 2^-64
+            r = 0x1p64f;
+        } else {
+            p = make_float2((float)(hr * pr - hi * pi), (float)(hr * pi + hi * pr));
+            r = (float)((-qr * pi + qi * pr) / (pi * pi + pr * pr));   // Re[(qr + i qi) / (-pi + i pr)]
+        }
     }
-    pq[m] = c;
+    reinterpret_cast<float2 *>(pq)[m] = p;
+    reinterpret_cast<float *>(pq)[2 * N + m] = r;
 }
 
 struct Launch {

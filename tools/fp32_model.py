@@ -214,8 +214,10 @@ def forward(frames, rand=False, twmode="rec", plain=False, r0=0):
     return Z
 
 
-def split_filter(Z, d, tb, Hd, exact=False):
-    """T[m] (inverse input m < N) = Zk P + conj(Zc) Q, (P, Q) in double rounded once"""
+def split_filter(Z, d, tb, Hd, exact=False, form="pr"):
+    """T[m] (inverse input m < N) = Zk P + conj(Zc) Q, the table in double rounded once.
+    form "pr" (round 6, split_pr): P and r = Q / (i P) as float, T = P (Zk + i r conj Zc); bin 2048
+    (P = 0) holds r = 2^64, P = Q / (i 2^64).  "pq" (round 5, split_pq): the (P, Q) float4."""
     N = HALF >> d
     m = np.arange(N)
     binv = tb + m - np.where(m >= N // 2, N, 0)
@@ -229,9 +231,18 @@ def split_filter(Z, d, tb, Hd, exact=False):
     zc = Z[:, (HALF - bb) % HALF]
     if exact:
         return zk * P + np.conj(zc) * Q
-    c = [P.real.astype(f32), P.imag.astype(f32), Q.real.astype(f32), Q.imag.astype(f32)]
     zkx, zky = zk.real.astype(f32), zk.imag.astype(f32)
     zcx, zcy = zc.real.astype(f32), zc.imag.astype(f32)
+    if form == "pr":
+        sp = ok & (bb == HALF // 2)
+        with np.errstate(divide="ignore", invalid="ignore"):
+            rr = np.where(ok & ~sp, ((1 + 1j * Wb) / (1j * (1 - 1j * Wb))).real, 0.0)
+        rr = np.where(sp, 2.0 ** 64, rr).astype(f32)
+        Pm = np.where(sp, Q / (1j * 2.0 ** 64), P)
+        px, py = Pm.real.astype(f32), Pm.imag.astype(f32)
+        vx, vy = fma(rr, zcy, zkx), fma(rr, zcx, zky)
+        return fma(vx, px, -(vy * py)).astype(f64) + 1j * fma(vx, py, vy * px).astype(f64)
+    c = [P.real.astype(f32), P.imag.astype(f32), Q.real.astype(f32), Q.imag.astype(f32)]
     # split_pq with contraction: x = ((zk.x c.x - zk.y c.y) + zc.x c.z) + zc.y c.w
     vx = fma(zcy, c[3], fma(zcx, c[2], fma(zkx, c[0], -(zky * c[1]))))
     vy = fma(-zcy, c[2], fma(zcx, c[3], fma(zkx, c[1], zky * c[0])))
@@ -262,7 +273,7 @@ def inverse_tail(T, N):
 
 
 def r2iq_model(stream, nblk, d, tb, lsb, rand, Hd, twmode="rec", plain=False, exact_fwd=False, exact_inv=False,
-               exact_split=False):
+               exact_split=False, split_form="pr"):
     """frames -> forward -> split -> inverse -> overlap-discard, as the kernels (d >= 3 tails)"""
     N = HALF >> d
     idx = np.array([BLOCK * b + HOP * k for b in range(nblk) for k in range(FRAMES)])
@@ -276,7 +287,7 @@ def r2iq_model(stream, nblk, d, tb, lsb, rand, Hd, twmode="rec", plain=False, ex
     else:
         r0 = (((tb - N // 2) % HALF) >> 8) if N <= 1024 else 0   # the pruned kernel's rotation
         Z = forward(frames, rand, twmode, plain, r0)
-    T = split_filter(Z, d, tb, Hd, exact_split)
+    T = split_filter(Z, d, tb, Hd, exact_split, split_form)
     if exact_inv:
         y = np.fft.ifft(T, axis=1) * N
     else:
@@ -304,7 +315,7 @@ def main():
         for name, kw in [("kernel", {}), ("fwd_table_tw", {"twmode": "table"}), ("anchor6", {"twmode": "anchor6"}),
                          ("fwd_plain16", {"plain": True}),
                          ("fwd_exact", {"exact_fwd": True}), ("inv_exact", {"exact_inv": True}),
-                         ("split_exact", {"exact_split": True}),
+                         ("split_exact", {"exact_split": True}), ("split_pq", {"split_form": "pq"}),
                          ("fwd_table_inv_exact", {"twmode": "table", "exact_inv": True})]:
             y = r2iq_model(x, nblk, d, tb, lsb, rand, H[d], **kw)
             row[name] = O.max_rel_err(y, ex)
