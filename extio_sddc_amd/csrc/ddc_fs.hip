@@ -242,6 +242,23 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
         for (int k = 0; k < 16; k++)
             if (!zrow<ZR>(k)) cr[k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rr, 4u * tid, 4u * NT * k, 0));
     }
+    // The plain static instances with zero rows (108-120 VGPRs before) also hold P of their first
+    // pairs p, 15 - p in registers: the |ZR| single-bin pairs (one row zero) and, at |ZR| = 4..7,
+    // one two-bin pair (at |ZR| = 7, 8 every live row; 122-126 VGPRs).  At tb 1024 (|ZR| = 4)
+    // 6 of 12 P loads per lane and frame stay: +1.4 %; |ZR| = 5..8: +1.2-2.7 %, bit-identical
+    // (profiles/r06/ab/fs_cached_p_*.txt)
+    constexpr int AZR = ZR > 0 ? ZR : -ZR;
+    constexpr int CPP = SCHED == kSchedStatic && !NCO && !CS16 && AZR >= 3 ? (AZR >= 4 && AZR <= 7 ? AZR + 1 : AZR) : 0;
+    float2 cp[16];
+    if constexpr (CPP > 0) {
+        const __amdgpu_buffer_rsrc_t rq = buf_rsrc(pqf);
+#pragma unroll
+        for (int k = 0; k < 16; k++)
+            if (!zrow<ZR>(k) && (k < CPP || 15 - k < CPP)) cp[k] = buf_load8(rq, 8u * tid, 8u * NT * k);
+    }
+    auto pload = [&](const __amdgpu_buffer_rsrc_t &rpq, unsigned t8p, int k) __attribute__((always_inline)) {
+        return (k < CPP || 15 - k < CPP) ? cp[k] : buf_load8(rpq, t8p, 8u * NT * k);
+    };
     constexpr bool GREG = SCHED == kSchedStatic;
     float2 cg0, cg1, cg4;
     if constexpr (GREG) {
@@ -330,8 +347,8 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
         float2 qa[8], qb[8];
 #pragma unroll
         for (int p = 0; p < kFsPqAhead; p++) {
-            if (!zrow<ZR>(p)) qa[p] = buf_load8(rpq, t8p, 8u * NT * p);
-            if (!zrow<ZR>(15 - p)) qb[p] = buf_load8(rpq, t8p, 8u * NT * (15 - p));
+            if (!zrow<ZR>(p)) qa[p] = pload(rpq, t8p, p);
+            if (!zrow<ZR>(15 - p)) qb[p] = pload(rpq, t8p, 15 - p);
         }
         asm volatile("" ::: "memory");
         {
@@ -360,8 +377,8 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
                 for (int p = 0; p < 8; p++) {
                     if (p + kFsPqAhead < 8) {
                         const int pn = p + kFsPqAhead;
-                        if (!zrow<ZR>(pn)) qa[pn] = buf_load8(rpq, t8p, 8u * NT * pn);
-                        if (!zrow<ZR>(15 - pn)) qb[pn] = buf_load8(rpq, t8p, 8u * NT * (15 - pn));
+                        if (!zrow<ZR>(pn)) qa[pn] = pload(rpq, t8p, pn);
+                        if (!zrow<ZR>(15 - pn)) qb[pn] = pload(rpq, t8p, 15 - pn);
                         asm volatile("" ::: "memory");
                     }
 #pragma unroll
@@ -384,8 +401,8 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
                 for (int p = 0; p < 8; p++) {
                     if (p + kFsPqAhead < 8) {
                         const int pn = p + kFsPqAhead;
-                        if (!zrow<ZR>(pn)) qa[pn] = buf_load8(rpq, t8p, 8u * NT * pn);
-                        if (!zrow<ZR>(15 - pn)) qb[pn] = buf_load8(rpq, t8p, 8u * NT * (15 - pn));
+                        if (!zrow<ZR>(pn)) qa[pn] = pload(rpq, t8p, pn);
+                        if (!zrow<ZR>(15 - pn)) qb[pn] = pload(rpq, t8p, 15 - pn);
                         asm volatile("" ::: "memory");
                     }
                     if (zrow<ZR>(15 - p)) {   // row 15 - p zero: row p's bin alone (v[15 - p] unwritten)
