@@ -102,6 +102,25 @@ def test_single_channel_parity(torch_dev, ddc, oracle, H, d, tb, lsb, rand, src)
     assert err <= TOL, f"max-rel-err {err:.3e} (rms {oracle.rms_rel_err(y, r):.3e})"
 
 
+# Tune bins that are not multiples of 4 (the C ABI takes any bin in [0, 4096); setFreqOffset only
+# produces multiples of 4, fft_mt_r2iq.cpp:104): at d = 0 they run the persistent kernel instead of
+# the FS kernel, with its forward pass 2 on the il272 columns and Z rotated by the tune bin.
+ODD_BINS = [(0, 1, 0, 0, "uniform"), (0, 1023, 1, 1, "mix"), (0, 2046, 0, 0, "uniform"), (0, 4095, 0, 1, "mix"),
+            (0, 2049, 1, 0, "uniform"), (1, 3, 0, 0, "mix"), (1, 2047, 1, 1, "uniform"), (2, 1021, 0, 0, "mix"),
+            (3, 2050, 0, 1, "uniform"), (6, 4093, 1, 0, "uniform")]
+
+
+@pytest.mark.parametrize("d,tb,lsb,rand,src", ODD_BINS)
+def test_tune_bins_not_multiple_of_4(torch_dev, ddc, oracle, H, d, tb, lsb, rand, src):
+    nblk = 3
+    x = make_stream(nblk, src)
+    y = run_device(torch_dev, ddc, x, nblk, d, tb, lsb, rand)
+    r = oracle.r2iq(x, nblk, d, tb, lsb, rand, H=H)
+    assert np.all(np.isfinite(y))
+    err = oracle.max_rel_err(y, r)
+    assert err <= TOL, f"max-rel-err {err:.3e}"
+
+
 def test_zero_input_gives_zero(torch_dev, ddc):
     y = run_device(torch_dev, ddc, make_stream(2, "zeros"), 2, 0, 1024, 0, 0)
     assert np.all(y == 0)
