@@ -254,11 +254,9 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
         const __amdgpu_buffer_rsrc_t rq = buf_rsrc(pqf);
 #pragma unroll
         for (int k = 0; k < 16; k++)
-            if (!zrow<ZR>(k) && (k < CPP || 15 - k < CPP)) cp[k] = buf_load8(rq, 8u * tid, 8u * NT * k);
+            if (!zrow<ZR>(k) && (k < CPP || 15 - k < CPP))
+                cp[k] = buf_load8(rq, 16u * tid, 4096u * (k < 8 ? k : 15 - k) + (k < 8 ? 0u : 8u));
     }
-    auto pload = [&](const __amdgpu_buffer_rsrc_t &rpq, unsigned t8p, int k) __attribute__((always_inline)) {
-        return (k < CPP || 15 - k < CPP) ? cp[k] : buf_load8(rpq, t8p, 8u * NT * k);
-    };
     constexpr bool GREG = SCHED == kSchedStatic;
     float2 cg0, cg1, cg4;
     if constexpr (GREG) {
@@ -343,12 +341,33 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
         // (an empty asm with a memory clobber pins each group; the compiler's own schedule waits
         // for every pair right after issuing it).
         const __amdgpu_buffer_rsrc_t rpq = buf_rsrc(pqf + z);
-        const unsigned t8p = 8u * (unsigned)t;
+        const unsigned t16 = 16u * (unsigned)t;
         float2 qa[8], qb[8];
+        // pair p's P (rows p and 15 - p side by side, build_fs_tables_kernel): one 16-byte load,
+        // or 8 bytes when a row is zero; the first CPP pairs from registers
+        // (8-byte halves where a 16-byte load would spill: ZR = +-2, the stealing schedule)
+        constexpr bool P16 = ZR != 2 && ZR != -2 && SCHED != kSchedSteal;
+        auto pload = [&](int p) __attribute__((always_inline)) {
+            const bool za = zrow<ZR>(p), zb = zrow<ZR>(15 - p);
+            if (p < CPP) {
+                if (!za) qa[p] = cp[p];
+                if (!zb) qb[p] = cp[15 - p];
+            } else if (!za && !zb && !P16) {
+                qa[p] = buf_load8(rpq, t16, 4096u * p);
+                qb[p] = buf_load8(rpq, t16, 4096u * p + 8u);
+            } else if (!za && !zb) {
+                const float4 q = buf_load16(rpq, t16, 4096u * p);
+                qa[p] = make_float2(q.x, q.y);
+                qb[p] = make_float2(q.z, q.w);
+            } else if (!za) {
+                qa[p] = buf_load8(rpq, t16, 4096u * p);
+            } else if (!zb) {
+                qb[p] = buf_load8(rpq, t16, 4096u * p + 8u);
+            }
+        };
 #pragma unroll
         for (int p = 0; p < kFsPqAhead; p++) {
-            if (!zrow<ZR>(p)) qa[p] = pload(rpq, t8p, p);
-            if (!zrow<ZR>(15 - p)) qb[p] = pload(rpq, t8p, 15 - p);
+            pload(p);
         }
         asm volatile("" ::: "memory");
         {
@@ -377,8 +396,7 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
                 for (int p = 0; p < 8; p++) {
                     if (p + kFsPqAhead < 8) {
                         const int pn = p + kFsPqAhead;
-                        if (!zrow<ZR>(pn)) qa[pn] = pload(rpq, t8p, pn);
-                        if (!zrow<ZR>(15 - pn)) qb[pn] = pload(rpq, t8p, 15 - pn);
+                        pload(pn);
                         asm volatile("" ::: "memory");
                     }
 #pragma unroll
@@ -401,8 +419,7 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
                 for (int p = 0; p < 8; p++) {
                     if (p + kFsPqAhead < 8) {
                         const int pn = p + kFsPqAhead;
-                        if (!zrow<ZR>(pn)) qa[pn] = pload(rpq, t8p, pn);
-                        if (!zrow<ZR>(15 - pn)) qb[pn] = pload(rpq, t8p, 15 - pn);
+                        pload(pn);
                         asm volatile("" ::: "memory");
                     }
                     if (zrow<ZR>(15 - p)) {   // row 15 - p zero: row p's bin alone (v[15 - p] unwritten)
@@ -543,7 +560,8 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
 }
 
 // FS tables of one tunebin, for lane l and row k (bin b = kFsPerm[l] + 256 k): P as float2 at
-// pqf[l + 256 k] (bytes 0 .. 32 K) and r as float at byte 32 K + 4 (l + 256 k) (inverse input
+// float2 index 2 (256 p + l) + [k >= 8], p = min(k, 15 - k), i.e. the pair's rows k, 15 - k side by
+// side for one 16-byte load (bytes 0 .. 32 K), and r as float at byte 32 K + 4 (l + 256 k) (inverse input
 // m = (b - tb) mod 4096; P and Q = i r P zero unless b is in the reference's band:
 // tb <= b < tb + 2048, b < 4096, or tb - 2048 <= b < tb).  With P = H (1 - i W), Q = H (1 + i W)
 // (H = H_0[m] / 2, W = e^{-2 pi i b / 8192}), r = Q / (i P) = (1 + i W) / (i (1 - i W))
@@ -579,7 +597,8 @@ __global__ void build_fs_tables_kernel(const float2 *__restrict__ hsel0, const f
             c.z = (float)((-qr * pi + qi * pr) / (pi * pi + pr * pr));
         }
     }
-    reinterpret_cast<float2 *>(pqf)[i] = make_float2(c.x, c.y);
+    // P of rows kk and 15 - kk side by side: float2 index 2 (256 p + l) + [kk >= 8], p = min(kk, 15 - kk)
+    reinterpret_cast<float2 *>(pqf)[2 * (NT * (kk < 8 ? kk : 15 - kk) + l) + (kk >= 8)] = make_float2(c.x, c.y);
     reinterpret_cast<float *>(pqf)[2 * HALF + i] = c.z;
     if (i < NT) {
         fsl[i] = tw4096[(tunebin * i) & (HALF - 1)];
