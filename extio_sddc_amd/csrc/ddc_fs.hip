@@ -234,7 +234,7 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
     // drops to 8 bytes per bin) and, for the static schedule, I2's lane factors g_t, g_t W^{-t},
     // g_t W^{-4t} (6 VGPRs; the queue and stealing schedules, at 124-128 VGPRs, keep the loads).
     // Per frame 12 KB of table reads fewer at tb = 1024: +2.5-3 % (profiles/r06/ab/
-    // fs_cached_r_and_lane_factors_*.txt).  118 VGPRs at ZR = 4.
+    // fs_cached_r_and_lane_factors_*.txt).  118 VGPRs at ZR = 4 (128 with the P pairs below).
     float cr[16];
     {
         const __amdgpu_buffer_rsrc_t rr = buf_rsrc(reinterpret_cast<const float *>(pqf) + 2 * HALF);
@@ -339,7 +339,8 @@ __global__ __launch_bounds__(NT, 4) void r2iq_fs_kernel(
         // The split's P loads (bin pairs p, 15 - p; 8 bytes per bin) run a pair ahead of their
         // use, the first issued before F2 so that its reads and arithmetic cover the L2 latency
         // (an empty asm with a memory clobber pins each group; the compiler's own schedule waits
-        // for every pair right after issuing it).
+        // for every pair right after issuing it).  Issuing the first pair after the register-held
+        // ones before F2 instead measured -2.4 to +0.9 % (fs_first_uncached_p_before_f2_NEUTRAL.txt).
         const __amdgpu_buffer_rsrc_t rpq = buf_rsrc(pqf + z);
         const unsigned t16 = 16u * (unsigned)t;
         float2 qa[8], qb[8];
