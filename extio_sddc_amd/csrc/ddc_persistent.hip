@@ -40,6 +40,21 @@ __device__ unsigned g_p_stamps[2048 * 4 * kStampWords];
 // free for every read and write pattern (tools/r4_tail_model.py, which also checks the passes
 // against numpy).  The [N/16, 16] form it replaces kept 16 lanes busy (d = 4) or fewer; its two
 // passes cost 8-11 % of the launch at d = 4..6 (timing-only build, profiles/r03/ab).
+// The split tables' layout (build_split_filter_kernel): for N >= 512 thread t's inverse inputs
+// m = t + 256 r sit so that each load is 16 bytes per lane and coalesced over the lanes: P of
+// (t, r) at float2 2 (256 (r >> 1) + t) + (r & 1) (pairs r, r + 1), r of (t, r) at float
+// 2 N + G (256 (r / G) + t) + r % G, G = min(R0, 4) (quads); N <= 256: at m.
+__host__ __device__ constexpr int pq_p_index(int N, int m)
+{
+    return N >= 512 ? 2 * (256 * ((m >> 8) >> 1) + (m & 255)) + ((m >> 8) & 1) : m;
+}
+__host__ __device__ constexpr int pq_r_index(int N, int m)
+{
+    return N >= 512 ? (N / 256 < 4 ? N / 256 : 4) * (256 * ((m >> 8) / (N / 256 < 4 ? N / 256 : 4)) + (m & 255))
+                          + (m >> 8) % (N / 256 < 4 ? N / 256 : 4)
+                    : m;
+}
+
 template <int N> constexpr int tail_radix(int p) { return N == 512 || (N == 128 && p == 0) ? 8 : 4; }
 template <int N> constexpr int tail_passes() { return N == 256 ? 4 : 3; }
 template <int N> constexpr int tail_ns(int p)
@@ -329,7 +344,7 @@ __global__ __launch_bounds__(NT, 4) void r2iq_persistent_kernel(
     if constexpr (RREG) {
         const float *rt = reinterpret_cast<const float *>(pq) + 2 * N;
 #pragma unroll
-        for (int r = 0; r < RR; r++) rreg[r] = (N >= 512 || tid < N) ? rt[tid + NT * r] : 0.f;
+        for (int r = 0; r < RR; r++) rreg[r] = (N >= 512 || tid < N) ? rt[pq_r_index(N, tid + NT * r)] : 0.f;
     }
 
     __syncthreads();   // s_first, s_next
@@ -447,8 +462,22 @@ __global__ __launch_bounds__(NT, 4) void r2iq_persistent_kernel(
                 const __amdgpu_buffer_rsrc_t rpq = buf_rsrc(pqz);
                 const __amdgpu_buffer_rsrc_t rrt = buf_rsrc(reinterpret_cast<const float *>(pqz) + 2 * N);
                 float2 a[R0];
+                constexpr int G = R0 < 4 ? R0 : 4;
+                float2 pp[2];
+                float rq[4];
 #pragma unroll
                 for (int r = 0; r < R0; r++) {
+                    if ((r & 1) == 0) {   // P of r, r + 1: one 16-byte load
+                        const float4 q = buf_load16(rpq, 2u * t8, 4096u * (unsigned)(r >> 1));
+                        pp[0] = make_float2(q.x, q.y);
+                        pp[1] = make_float2(q.z, q.w);
+                    }
+                    if constexpr (!RREG) {
+                        if (r % G == 0) {   // r of r .. r + 3: one 16-byte load
+                            const float4 q = buf_load16(rrt, 2u * t8, 4096u * (unsigned)(r / G));
+                            rq[0] = q.x, rq[1] = q.y, rq[2] = q.z, rq[3] = q.w;
+                        }
+                    }
                     const bool wrap = (NT * r >= N / 2);
                     const int sh = NT * r - (wrap ? N : 0);
                     // branch-free: read a valid (wrapped) address, out-of-band bins have P = Q = 0;
@@ -459,8 +488,7 @@ __global__ __launch_bounds__(NT, 4) void r2iq_persistent_kernel(
                     else if constexpr (ZROT) zk = w0[t + (sh & (HALF - 1))];
                     else zk = *reinterpret_cast<const float2 *>(w0b + ((sb0b + 8u * (unsigned)sh) & (8u * HALF - 8u)));
                     const float2 zc = *reinterpret_cast<const float2 *>(w0b + ((sc0b - 8u * (unsigned)sh) & (8u * HALF - 8u)));
-                    const float rv = RREG ? rreg[r] : __int_as_float(buf_load4(rrt, t8 >> 1, 4u * NT * r));
-                    a[r] = split_pr(zk, zc, buf_load8(rpq, t8, 8u * NT * r), rv);
+                    a[r] = split_pr(zk, zc, pp[r & 1], RREG ? rreg[r] : rq[r % G]);
                 }
                 if constexpr (WGT) {
                     constexpr int B = N / 1024, T = N / 4;
@@ -634,8 +662,8 @@ __global__ __launch_bounds__(NT, 4) void r2iq_persistent_kernel(
 
 // ---------------------------------------------------------------------------------------------
 // Split x filter coefficients for one (d, tunebin), inverse input m (bin = tb + m - (m >= N/2 ? N : 0),
-// fft_mt_r2iq_impl.hpp:84-98; zero outside [0, 4096)): P as float2 at pq[m] (bytes 0 .. 8 N) and
-// r = Q / (i P) as float at float index 2 N + m (split_pr).  r is infinite at bin 2048 (P = 0,
+// fft_mt_r2iq_impl.hpp:84-98; zero outside [0, 4096)): P as float2 (bytes 0 .. 8 N) and
+// r = Q / (i P) as float from float index 2 N (split_pr), at pq_p_index / pq_r_index.  r is infinite at bin 2048 (P = 0,
 // X Hh = Q conj Zc): there r = 2^64 and P = Q / (i 2^64), exact power-of-two scalings, so that
 // P (Zk + i r conj Zc) = Q conj Zc - i 2^-64 Q Zk, the second term far below float32's resolution
 // of the first (|Zc| < 2^28: no overflow).  Evaluated in double from the float tables and rounded once.
@@ -662,8 +690,8 @@ __global__ void build_split_filter_kernel(const float2 *__restrict__ hsel, const
             r = (float)((-qr * pi + qi * pr) / (pi * pi + pr * pr));   // Re[(qr + i qi) / (-pi + i pr)]
         }
     }
-    reinterpret_cast<float2 *>(pq)[m] = p;
-    reinterpret_cast<float *>(pq)[2 * N + m] = r;
+    reinterpret_cast<float2 *>(pq)[pq_p_index(N, m)] = p;
+    reinterpret_cast<float *>(pq)[2 * N + pq_r_index(N, m)] = r;
 }
 
 struct Launch {
