@@ -183,13 +183,19 @@ __device__ __forceinline__ void tail_pass(float2 *sb, const float2 *twq, int t, 
     const int kk = t & (NS - 1);
     if (t < T) {
         float2 a[R];
-        // reads t + T r: t < T, so the two terms share no bit
+        // reads t + T r: t < T, so the two terms share no bit.  Data and twiddle reads each one
+        // ds_read_b64 (XRD; the compiler's ds_read2(st64)_b64 pairs take 8 LDS cycles against
+        // 2 per ds_read_b64): d = 4 +1.2 to +2.0 %, d = 3 -0.2 to +2.1 %, d = 5 +1.3 %, d = 6
+        // -0.3 %, bit-identical (profiles/r06/ab/persistent_tail_single_b64_reads.txt)
         const unsigned rd8 = 8u * (unsigned)tail_swz<N>(t);
 #pragma unroll
-        for (int r = 0; r < R; r++) a[r] = tail_x<N>(sb, rd8, T * r);
+        for (int r = 0; r < R; r++) XRD(a[r], tail_x<N>(sb, rd8, T * r));
         if constexpr (P > 0) {
+            float2 w[R];
 #pragma unroll
-            for (int r = 1; r < R; r++) a[r] = TW<+1>(a[r], twq[tail_twoff<N>(P) + (r - 1) * NS + kk]);
+            for (int r = 1; r < R; r++) XRD(w[r], twq[tail_twoff<N>(P) + (r - 1) * NS + kk]);
+#pragma unroll
+            for (int r = 1; r < R; r++) a[r] = TW<+1>(a[r], w[r]);
         }
         if constexpr (R == 8) dft8<+1>(a, u);
         else dft4<+1>(a, u);
