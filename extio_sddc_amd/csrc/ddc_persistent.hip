@@ -448,7 +448,13 @@ __global__ __launch_bounds__(NT, 4) void r2iq_persistent_kernel(
         } else {
             const int sZ = (t - zd) & 255;
 #pragma unroll
-            for (int r = 0; r < 16; r++) w0[sZ + NT * r] = v[r];   // Z, rotated by tb
+            // Z, rotated by tb: one ds_write_b64 per register (not the compiler's ds_write2st64_b64
+            // pairs): d = 1 +1.6 / +2.1 %, C4 +1.0 / +1.2 %, bit-identical
+            // (profiles/r06/ab/persistent_d1_single_z_stores.txt)
+            for (int r = 0; r < 16; r++) {
+                w0[sZ + NT * r] = v[r];
+                asm volatile("" ::: "memory");
+            }
         }
         if (tid == QLANE)   // the frame after the next one (read by every wave at the next frame's start)
             s_next = fn >= 0 && fn + 1 < f1s ? fn + 1 : -1;
