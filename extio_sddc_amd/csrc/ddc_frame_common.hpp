@@ -148,8 +148,14 @@ __device__ __forceinline__ void table_twiddle(float2 *a, const float2 *tbl, int 
 #pragma unroll
         for (int r = 9; r < 16; r++) a[r] = TW<DIR>(a[r], tw[r - 1]);
     } else {
+        // unpaired too (no ds_read2_b64): d = 2 +1.6 / +2.0 %, d = 3 +0.8 / +1.1 %, d = 4..6 -0.3 to
+        // +0.7 % (profiles/r06/ab/persistent_pass1_twiddles_unpaired_d2_6.txt)
 #pragma unroll
-        for (int r = 1; r < 16; r++) a[r] = TW<DIR>(a[r], tbl[(r - 1) * S + j]);
+        for (int r = 1; r < 16; r++) {
+            float2 w;
+            XRD(w, tbl[(r - 1) * S + j]);
+            a[r] = TW<DIR>(a[r], w);
+        }
     }
 }
 
